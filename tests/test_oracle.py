@@ -1,0 +1,157 @@
+"""CPU oracle: pinned against the reference kernels' own outputs (tests/golden)
+and against hand-derived known answers from the reference source."""
+import glob
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+TAGS = {"FULL_2CP": (0, 2), "FULL_3CP": (0, 3), "HALF_2CP": (1, 2), "HALF_3CP": (1, 3)}
+
+
+def cpmv6(cp):
+    return np.stack([cp[f] for f in ("LTx", "LTy", "RTx", "RTy", "LBx", "LBy")], 1)
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
+def test_oracle_matches_reference_golden(path):
+    z = np.load(path)
+    ref, cur, lam, extra = z["ref"], z["cur"], float(z["lam"]), int(z["extra"])
+    for align in (0, 1):
+        base = "FULL" if align == 0 else "HALF"
+        c2, p2 = O.affine_me(ref, cur, lam, align, 2, extra)
+        np.testing.assert_array_equal(c2, z[base + "_2CP_cost"])
+        np.testing.assert_array_equal(cpmv6(p2), z[base + "_2CP_cpmv"])
+        # 3-CP seeded from the REFERENCE's own 2-CP output (affine.cl:81)
+        prev = np.zeros(c2.size, O.CPMVS_DTYPE)
+        for i, f in enumerate(("LTx", "LTy", "RTx", "RTy", "LBx", "LBy")):
+            prev[f] = z[base + "_2CP_cpmv"][:, i]
+        c3, p3 = O.affine_me(ref, cur, lam, align, 3, extra, prev=prev)
+        np.testing.assert_array_equal(c3, z[base + "_3CP_cost"])
+        np.testing.assert_array_equal(cpmv6(p3), z[base + "_3CP_cpmv"])
+
+
+def test_golden_set_present():
+    assert len(GOLDEN) >= 10
+
+
+def test_kat1_integer_mv_filter_is_identity():
+    # aux_functions.cl:1124-1223: frac 0 -> (64s-32768)>>2 = 16s-8192 -> s
+    rng = np.random.default_rng(1)
+    ref = rng.integers(0, 1024, (240, 416)).astype(np.uint16)
+    out = np.zeros(16, np.int32)
+    for (x, y, mvx, mvy) in [(100, 60, 0, 0), (0, 0, 0, 0), (412, 236, 0, 0), (40, 40, 32, -48)]:
+        O.lib().vame_oracle_predict_4x4(O.ptr(ref), 416, 240, x, y, mvx, mvy, O.ptr(out))
+        xs = np.clip(np.arange(x, x + 4) + mvx // 16, 0, 415)
+        ys = np.clip(np.arange(y, y + 4) + mvy // 16, 0, 239)
+        np.testing.assert_array_equal(out.reshape(4, 4), ref[np.ix_(ys, xs)])
+
+
+def test_kat4_satd():
+    a = np.full(16, 5, np.int32)
+    assert O.lib().vame_oracle_satd4x4(O.ptr(a + 1), O.ptr(a)) == 2
+    assert O.lib().vame_oracle_satd4x4(O.ptr(a), O.ptr(a)) == 0
+
+
+@pytest.mark.parametrize("v,bits", [(0, 1), (1, 3), (-1, 3), (2, 5), (64, 15), (65, 15),
+                                    (-64, 15), (8192, 29)])
+def test_kat5_expgolomb(v, bits):
+    assert O.lib().vame_oracle_eg_bits(v) == bits
+
+
+@pytest.mark.parametrize("v,q", [(1, 0), (2, 0), (3, 1), (5, 1), (7, 2), (-1, 0), (-2, 0),
+                                 (-3, -1), (-5, -1), (-7, -2), (0, 0)])
+def test_kat6_quarter_rounding(v, q):
+    assert O.lib().vame_oracle_to_quarter(v) == q
+
+
+def test_t6_double_to_int_follows_gpu_cvt():
+    L = O.lib()
+    assert L.vame_oracle_scale_delta(float("nan")) == 0
+    assert L.vame_oracle_scale_delta(1e300) == -4          # INT_MAX << 2 wraps
+    assert L.vame_oracle_scale_delta(-1e300) == 0          # INT_MIN << 2 wraps
+    assert L.vame_oracle_scale_delta(0.0) == 0             # (int)(0 + 0.5) = 0
+    assert L.vame_oracle_scale_delta(0.13) == 4            # (int)(0.52+0.5) = 1 -> 4
+    assert L.vame_oracle_scale_delta(-0.13) == -4
+
+
+def test_t7_rate_cost_single_precision():
+    lam = np.float32(78.949063)
+    for bits in (6, 8, 17, 123):
+        assert O.lib().vame_oracle_rate_cost(bits, float(lam)) == math.floor(np.float32(lam * np.float32(bits)))
+    assert O.lib().vame_oracle_rate_cost(6, 78.949063) == 473
+    assert O.lib().vame_oracle_rate_cost(8, 78.949063) == 631
+
+
+def test_kat7_singular_system_gives_zero_update():
+    a = np.zeros((7, 7))
+    p = np.ones(6)
+    O.lib().vame_oracle_solve(O.ptr(a), 4, O.ptr(p))
+    assert (p[:4] == 0).all()
+
+
+def test_kat2_identical_frames():
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "s416_identical.npz"))
+    c, p = O.affine_me(z["ref"], z["cur"], float(z["lam"]), 0, 2)
+    assert (c == 473).all() and (cpmv6(p) == 0).all()
+
+
+def test_kat3_out_of_frame_rows():
+    # 416x240: CTU column 3 holds 32 px; rows of CUs not fully inside are logged
+    # with zero CPMVs and floor(lambda*6) (2 CP, affine.cl:192/208 + T9)
+    rng = np.random.default_rng(3)
+    ref = rng.integers(0, 1024, (240, 416)).astype(np.uint16)
+    cur = rng.integers(0, 1024, (240, 416)).astype(np.uint16)
+    c, p = O.affine_me(ref, cur, 78.949063, 0, 2)
+    geo = group_geometry(0)
+    n_out = 0
+    for ctu in range(8):
+        cx0, cy0 = (ctu % 4) * 128, (ctu // 4) * 128
+        for g, (w, h, xs, ys, stride) in enumerate(geo):
+            for k in range(len(xs)):
+                if cx0 + xs[k] + w > 416 or cy0 + ys[k] + h > 240:
+                    idx = ctu * 201 + stride + k
+                    assert c[idx] == 473 and (cpmv6(p[idx:idx + 1]) == 0).all()
+                    n_out += 1
+    assert n_out > 0
+
+
+def group_geometry(align):
+    out = []
+    for g in range(24 if align else 12):
+        w, h, n, s = (np.zeros(1, np.int32) for _ in range(4))
+        xs, ys = np.zeros(64, np.int32), np.zeros(64, np.int32)
+        assert O.lib().vame_oracle_group_geometry(align, g, O.ptr(w), O.ptr(h), O.ptr(n),
+                                                  O.ptr(s), O.ptr(xs), O.ptr(ys)) == 0
+        out.append((int(w[0]), int(h[0]), xs[:n[0]].copy(), ys[:n[0]].copy(), int(s[0])))
+    return out
+
+
+@pytest.mark.parametrize("align,total", [(0, 201), (1, 284)])
+def test_geometry_tables(align, total):
+    geo = group_geometry(align)
+    strides = [g[4] for g in geo]
+    counts = [len(g[2]) for g in geo]
+    assert strides == list(np.cumsum([0] + counts[:-1]))
+    assert sum(counts) == total
+    for (w, h, xs, ys, _) in geo:
+        cover = np.zeros((128, 128), np.int32)
+        for x, y in zip(xs, ys):
+            assert x % 8 == 0 and y % 8 == 0 and x + w <= 128 and y + h <= 128
+            # every CU sits inside one 64x64 quadrant unless it is a 128-wide/high CU
+            if w <= 64 and h <= 64:
+                assert x // 64 == (x + w - 1) // 64 and y // 64 == (y + h - 1) // 64
+            cover[y:y + h, x:x + w] += 1
+        assert cover.max() == 1  # CUs of one group never overlap
+
+
+def test_oracle_deterministic_across_threads():
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "s416_qp32_poc1_ref0.npz"))
+    a = O.affine_me(z["ref"], z["cur"], float(z["lam"]), 1, 2, nthreads=1)
+    b = O.affine_me(z["ref"], z["cur"], float(z["lam"]), 1, 2, nthreads=4)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(cpmv6(a[1]), cpmv6(b[1]))
