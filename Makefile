@@ -1,0 +1,45 @@
+# vame -- MI355X affine-ME engine.  `make` builds everything in-tree:
+#   vvc-affine-gpu_amd/lib/libvame.so   HIP kernels (gfx950) + C ABI (include/vame.h)
+#   vvc-affine-gpu_amd/bin/vame         C++ CLI, drop-in for the reference's ./main
+#   oracle/libvame_oracle.so            CPU restatement (tests / CPU baseline only)
+#   oracle/_ref/*                       reference kernels + harness (only where /root/reference exists)
+
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+PKG     := vvc-affine-gpu_amd
+CSRC    := $(PKG)/csrc
+LIBDIR  := $(PKG)/lib
+BINDIR  := $(PKG)/bin
+# -ffp-contract=off: the FP64 solve must round exactly like the reference
+# (explicit fma where OpenCL's FP_CONTRACT fuses); integer paths are unaffected.
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+
+LIB_SRCS := $(CSRC)/vame_engine.hip $(CSRC)/vame_hostlogic.cpp
+LIB_HDRS := $(CSRC)/vame_kernel.h $(CSRC)/vame_tables.h include/vame.h
+
+all: lib cli oracle
+
+lib: $(LIBDIR)/libvame.so
+cli: $(BINDIR)/vame
+
+$(LIBDIR)/libvame.so: $(LIB_SRCS) $(LIB_HDRS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(LIB_SRCS)
+
+$(BINDIR)/vame: $(PKG)/host/vame_main.cpp $(PKG)/host/vame_io.cpp $(PKG)/host/vame_io.h $(LIBDIR)/libvame.so
+	@mkdir -p $(BINDIR)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $(PKG)/host/vame_main.cpp $(PKG)/host/vame_io.cpp \
+	    -L$(LIBDIR) -lvame -Wl,-rpath,'$$ORIGIN/../lib' -lpthread
+
+oracle:
+	$(MAKE) -s -C oracle libvame_oracle.so
+	@if [ -d /root/reference ]; then $(MAKE) -s -C oracle ref; fi
+
+resource-usage:
+	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c -o /dev/null $(CSRC)/vame_engine.hip
+
+clean:
+	rm -rf $(LIBDIR) $(BINDIR)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all lib cli oracle clean resource-usage

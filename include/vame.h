@@ -1,0 +1,102 @@
+/*
+ * vame.h -- C ABI of the MI355X affine motion-estimation engine (libvame.so).
+ *
+ * Drop-in boundary for the reference's hot path (iagostorch/VVC-Affine-GPU):
+ * what the reference host does with clSetKernelArg + clEnqueueNDRangeKernel on
+ *   affine_gradient_mult_sizes     (affine.cl:11,  aligned CUs)      and
+ *   affine_gradient_mult_sizes_HA  (affine.cl:960, half-aligned CUs)
+ * compiled with -DnCP=2|3 (main.cpp:389-392) and launched at main.cpp:827-966
+ * is one call of vame_affine_me() here.  The gradient / equation scratch
+ * buffers of the reference signature (args 5-7) and its unused debug args
+ * (11-12) disappear: all scratch lives in LDS and registers.
+ *
+ * Plain pointers and sizes only.  Frame / result pointers are DEVICE pointers
+ * (hipMalloc'd or torch.cuda tensors) unless a function says otherwise; every
+ * call is asynchronous on `stream` (a hipStream_t, NULL = default stream).
+ * Results use the reference's return-array layout (affine.cl:936, :1929):
+ *   index = ctu * {201 | 284} + RETURN_STRIDE[group] + cuIdx
+ * so the host's decision-log writer (main_aux_functions.h:387-525) is unchanged.
+ * A context is bound to one device and is not thread-safe; use one per GPU per
+ * host thread.  Functions return 0 or a negative VAME_E* code.
+ */
+#ifndef VAME_H
+#define VAME_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* typedef.h:1-8 Mv / Cpmvs, same 28-byte layout.  1/16-pel units. */
+typedef struct { int32_t x, y; } vame_mv;
+typedef struct { int32_t nCPs; vame_mv LT, RT, LB; } vame_cpmvs;
+
+enum { VAME_ALIGN_FULL = 0, VAME_ALIGN_HALF = 1 };
+enum { VAME_MODE_2CP = 1, VAME_MODE_3CP = 2 }; /* mode_mask bits; 3CP requires 2CP */
+
+enum {
+  VAME_OK = 0,
+  VAME_E_INVALID = -1,     /* bad argument (resolution, nCP, align, null pointer ...) */
+  VAME_E_DEVICE = -2,      /* HIP runtime error (see vame_last_hip_error) */
+  VAME_E_NOMEM = -3,
+  VAME_E_UNSUPPORTED = -4  /* e.g. more than 4 reference frames */
+};
+
+typedef struct vame_ctx vame_ctx;
+
+/* Output slots of the fused per-POC call: [ref][FULL_2CP, FULL_3CP, HALF_2CP, HALF_3CP].
+ * cost/cpmvs of slot (r, m) must hold nCtus*{201|284} entries (or be NULL when the
+ * mode is not requested).  Mirrors the four return_* memory objects per refIdx
+ * of main.cpp:484-504. */
+typedef struct {
+  int64_t* cost[4][4];
+  vame_cpmvs* cpmvs[4][4];
+} vame_poc_result;
+
+/* Create a context on HIP device `device` for frames of width x height (one of
+ * the reference's resolutions: constants.h:73-79 / main.cpp:257-265). */
+int vame_create(vame_ctx** out, int device, int width, int height);
+void vame_destroy(vame_ctx* ctx);
+
+/* One reference launch (affine.cl:11 or :960 built with -DnCP=nCP).
+ *   ref, cur : W*H uint16 samples (10-bit), device memory
+ *   lambda   : motion lambda (float kernel arg 4, main.cpp:585/831)
+ *   prev     : nCP==3 only: the same-alignment 2-CP result of this (POC, ref)
+ *              (gPrevCpmvs, main.cpp:777/908); NULL for nCP==2
+ *   cost     : nCtus*{201|284} int64 best RD cost per candidate CU
+ *   cpmvs    : same count, best CPMVs (LB = 0 for 2 CPs)                       */
+int vame_affine_me(vame_ctx* ctx, const uint16_t* ref, const uint16_t* cur, float lambda,
+                   int align, int nCP, int extra_grad_iter, const vame_cpmvs* prev,
+                   int64_t* cost, vame_cpmvs* cpmvs, void* stream);
+
+/* Fused per-POC call: every ref x {FULL, HALF} x {2CP -> 3CP} in one pass
+ * (the whole refIdx loop of main.cpp:746-966).  3-CP seeds come from the 2-CP
+ * result of the same CU inside the kernel (no round trip through memory). */
+int vame_affine_me_poc(vame_ctx* ctx, const uint16_t* cur, const uint16_t* const* refs,
+                       int nrefs, float lambda, int mode_mask, int extra_grad_iter,
+                       const vame_poc_result* out, void* stream);
+
+/* Geometry / host helpers (no device work). */
+int vame_num_ctus(int width, int height);   /* 0 if unsupported */
+int vame_cus_per_ctu(int align);            /* 201 / 284 */
+int vame_num_groups(int align);             /* 12 / 24 */
+/* CU group g: size, count, return stride, CTU-relative positions (xs/ys >= 64 entries) */
+int vame_group_geometry(int align, int g, int* w, int* h, int* ncu, int* stride, int* xs,
+                        int* ys);
+/* Motion lambda of a POC (main.cpp:585 -> main_aux_functions.h:1482-1497, constants.h:94-103) */
+float vame_lambda(int qp, int poc);
+int vame_poc_qp(int qp, int poc);
+/* Reference-picture list of a POC (main.cpp:591-707): fills pocs[0..min(4,poc)-1]
+ * with the POC held by each refIdx slot; returns the number of refs. */
+int vame_ref_list(int poc, int* pocs);
+
+const char* vame_strerror(int code);
+const char* vame_last_hip_error(void);
+const char* vame_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VAME_H */

@@ -1,0 +1,139 @@
+"""HIP path (libvame.so, called through the C ABI) vs the reference kernels'
+golden outputs and vs the pinned CPU oracle.  Bit-exact: every cost and every
+CPMV component of every candidate CU."""
+import glob
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+MODES = {"FULL_2CP": (0, 2), "FULL_3CP": (0, 3), "HALF_2CP": (1, 2), "HALF_3CP": (1, 3)}
+
+
+@pytest.fixture(scope="module")
+def engines():
+    from vame.engine import Engine
+    cache = {}
+
+    def get(W, H):
+        if (W, H) not in cache:
+            cache[(W, H)] = Engine(W, H, 0)
+        return cache[(W, H)]
+    yield get
+    for e in cache.values():
+        e.close()
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).cuda()
+
+
+def host(res):
+    cost, cp = res
+    torch.cuda.synchronize()
+    return cost.cpu().numpy(), cp.cpu().numpy()
+
+
+def cp6(cp):
+    return cp[:, 1:7]
+
+
+def oracle_cp6(cp):
+    return np.stack([cp[f] for f in ("LTx", "LTy", "RTx", "RTy", "LBx", "LBy")], 1)
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
+def test_dropin_launches_match_reference(engines, path):
+    """vame_affine_me == one reference launch, for each of the 4 kernel objects."""
+    z = np.load(path)
+    W, H = int(z["W"]), int(z["H"])
+    eng = engines(W, H)
+    ref, cur = dev(z["ref"]), dev(z["cur"])
+    lam, extra = float(z["lam"]), int(z["extra"])
+    for align, base in ((0, "FULL"), (1, "HALF")):
+        c2, p2 = eng.affine_me(ref, cur, lam, align, 2, extra)
+        hc2, hp2 = host((c2, p2))
+        np.testing.assert_array_equal(hc2, z[base + "_2CP_cost"], err_msg=f"{base} 2CP cost")
+        np.testing.assert_array_equal(cp6(hp2), z[base + "_2CP_cpmv"], err_msg=f"{base} 2CP cpmv")
+        assert (hp2[:, 0] == 2).all()
+        c3, p3 = eng.affine_me(ref, cur, lam, align, 3, extra, prev=p2)
+        hc3, hp3 = host((c3, p3))
+        np.testing.assert_array_equal(hc3, z[base + "_3CP_cost"], err_msg=f"{base} 3CP cost")
+        np.testing.assert_array_equal(cp6(hp3), z[base + "_3CP_cpmv"], err_msg=f"{base} 3CP cpmv")
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
+def test_fused_poc_matches_reference(engines, path):
+    """vame_affine_me_poc (all modes, 3-CP chained in-kernel) == the 4 reference launches."""
+    z = np.load(path)
+    W, H = int(z["W"]), int(z["H"])
+    eng = engines(W, H)
+    ref, cur = dev(z["ref"]), dev(z["cur"])
+    out = eng.affine_me_poc(cur, [ref, ref], float(z["lam"]), modes=3, extra=int(z["extra"]))
+    for r in (0, 1):
+        for name in MODES:
+            hc, hp = host(out[(r, name)])
+            np.testing.assert_array_equal(hc, z[name + "_cost"], err_msg=f"ref{r} {name}")
+            np.testing.assert_array_equal(cp6(hp), z[name + "_cpmv"], err_msg=f"ref{r} {name}")
+
+
+@pytest.mark.parametrize("W,H", [(1920, 1080), (1280, 720)])
+def test_fused_vs_oracle_synthetic(engines, W, H):
+    from vame import synth
+    o, r = synth.synth_sequence(W, H, 2, 32)
+    eng = engines(W, H)
+    lam = 70.335619
+    out = eng.affine_me_poc(dev(o[1]), [dev(r[1]), dev(r[0])], lam, modes=3)
+    for ri, refr in enumerate((r[1], r[0])):
+        want = O.affine_me_pair(refr, o[1], lam)
+        for name, key in MODES.items():
+            hc, hp = host(out[(ri, name)])
+            oc, op = want[key]
+            np.testing.assert_array_equal(hc, oc, err_msg=f"{W}x{H} ref{ri} {name}")
+            np.testing.assert_array_equal(cp6(hp), oracle_cp6(op), err_msg=f"{W}x{H} ref{ri} {name}")
+
+
+def test_2cp_only_mode(engines):
+    z = np.load(GOLDEN[0])
+    eng = engines(int(z["W"]), int(z["H"]))
+    out = eng.affine_me_poc(dev(z["cur"]), [dev(z["ref"])], float(z["lam"]), modes=1,
+                            extra=int(z["extra"]))
+    assert set(out) == {(0, "FULL_2CP"), (0, "HALF_2CP")}
+    for name in ("FULL_2CP", "HALF_2CP"):
+        hc, hp = host(out[(0, name)])
+        np.testing.assert_array_equal(hc, z[name + "_cost"])
+
+
+REF_HARNESS = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle", "_ref", "ref_harness_hip")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_HARNESS), reason="reference kernels not built")
+def test_live_reference_1080p(engines, tmp_path):
+    """The reference kernels themselves, run on this GPU, vs the HIP path at 1080p."""
+    from vame import synth
+    o, r = synth.synth_sequence(1920, 1080, 1, 32, seed=0xABCD)
+    lam = 78.949063
+    r[0].tofile(tmp_path / "ref.u16")
+    o[0].tofile(tmp_path / "cur.u16")
+    (tmp_path / "jobs.txt").write_text(
+        f"1920 1080 {lam!r} 0 {tmp_path / 'ref.u16'} {tmp_path / 'cur.u16'} {tmp_path / 'p'}\n")
+    d = os.path.dirname(REF_HARNESS)
+    subprocess.run([REF_HARNESS, os.path.join(d, "affine_2cp.co"), os.path.join(d, "affine_3cp.co"),
+                    str(tmp_path / "jobs.txt")], check=True, timeout=300, capture_output=True)
+    eng = engines(1920, 1080)
+    out = eng.affine_me_poc(dev(o[0]), [dev(r[0])], lam, modes=3)
+    for name in MODES:
+        n = 135 * (201 if name.startswith("FULL") else 284)
+        raw = np.fromfile(tmp_path / f"p_{name}.bin", np.uint8)
+        cost = raw[:n * 8].view(np.int64)
+        cp = raw[n * 8:].view(np.int32).reshape(n, 7)
+        hc, hp = host(out[(0, name)])
+        np.testing.assert_array_equal(hc, cost, err_msg=name)
+        np.testing.assert_array_equal(cp6(hp), cp[:, 1:], err_msg=name)

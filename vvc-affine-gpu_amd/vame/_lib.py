@@ -1,0 +1,62 @@
+"""ctypes binding of libvame.so (include/vame.h).  Fails loudly when the
+library is missing -- there is no fallback implementation."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("VAME_LIB", os.path.join(PKG_DIR, "lib", "libvame.so"))
+
+# every symbol include/vame.h declares
+EXPORTS = (
+    "vame_create", "vame_destroy", "vame_affine_me", "vame_affine_me_poc", "vame_num_ctus",
+    "vame_cus_per_ctu", "vame_num_groups", "vame_group_geometry", "vame_lambda", "vame_poc_qp",
+    "vame_ref_list", "vame_strerror", "vame_last_hip_error", "vame_version",
+)
+
+
+class VameError(RuntimeError):
+    pass
+
+
+class PocResult(ctypes.Structure):
+    _fields_ = [("cost", (ctypes.c_void_p * 4) * 4), ("cpmvs", (ctypes.c_void_p * 4) * 4)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise VameError(f"libvame.so not built ({LIB_PATH}); run `make` at the repo root")
+        L = ctypes.CDLL(LIB_PATH)
+        P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        L.vame_create.argtypes = [ctypes.POINTER(P), I, I, I]
+        L.vame_destroy.argtypes = [P]
+        L.vame_destroy.restype = None
+        L.vame_affine_me.argtypes = [P, P, P, F, I, I, I, P, P, P, P]
+        L.vame_affine_me_poc.argtypes = [P, P, P, I, F, I, I, ctypes.POINTER(PocResult), P]
+        L.vame_num_ctus.argtypes = [I, I]
+        L.vame_cus_per_ctu.argtypes = [I]
+        L.vame_num_groups.argtypes = [I]
+        L.vame_group_geometry.argtypes = [I, I, P, P, P, P, P, P]
+        L.vame_lambda.argtypes = [I, I]
+        L.vame_lambda.restype = F
+        L.vame_poc_qp.argtypes = [I, I]
+        L.vame_ref_list.argtypes = [I, P]
+        L.vame_strerror.argtypes = [I]
+        L.vame_strerror.restype = ctypes.c_char_p
+        L.vame_last_hip_error.restype = ctypes.c_char_p
+        L.vame_version.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        L = lib()
+        raise VameError(f"vame error {rc}: {L.vame_strerror(rc).decode()} "
+                        f"{L.vame_last_hip_error().decode()}")

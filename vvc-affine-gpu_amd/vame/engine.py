@@ -1,0 +1,101 @@
+"""Device-side entry points (HIP kernels via libvame.so) on torch.cuda tensors.
+
+Mirrors the reference's operator interface for this path:
+  * `Engine.affine_me(ref, cur, lam, align, ncp, extra, prev)` == one launch of
+    affine_gradient_mult_sizes(_HA) built with -DnCP=ncp (affine.cl:11/:960,
+    args set at main.cpp:827-840), returning the gBestCost / gBestCpmvs arrays;
+  * `Engine.affine_me_poc(cur, refs, lam, ...)` == the whole refIdx loop of one
+    POC (main.cpp:746-966), fused into one pass.
+Frames are (H, W) int16/uint16 tensors of 10-bit samples on the engine's device.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from ._lib import PocResult, check, lib
+
+CPMV_FIELDS = ("nCPs", "LTx", "LTy", "RTx", "RTy", "LBx", "LBy")
+MODES = ("FULL_2CP", "FULL_3CP", "HALF_2CP", "HALF_3CP")
+
+
+def _ptr(t: torch.Tensor | None):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class Engine:
+    def __init__(self, width: int, height: int, device: int | torch.device = 0):
+        if not torch.cuda.is_available():
+            raise RuntimeError("vame.Engine needs a HIP device (no CPU fallback)")
+        self.device = torch.device("cuda", device if isinstance(device, int) else device.index)
+        self.W, self.H = width, height
+        self.n_ctus = lib().vame_num_ctus(width, height)
+        if not self.n_ctus:
+            raise ValueError(f"unsupported resolution {width}x{height}")
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().vame_create(ctypes.byref(h), self.device.index, width, height))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().vame_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def n_cus(self, align: int) -> int:
+        return self.n_ctus * (284 if align else 201)
+
+    def _frame(self, f: torch.Tensor) -> torch.Tensor:
+        if f.shape != (self.H, self.W) or f.device != self.device or f.dtype not in (torch.int16, torch.uint16):
+            raise ValueError(f"frame must be ({self.H},{self.W}) int16/uint16 on {self.device}")
+        return f.contiguous()
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def alloc_result(self, align: int):
+        n = self.n_cus(align)
+        return (torch.empty(n, dtype=torch.int64, device=self.device),
+                torch.empty((n, 7), dtype=torch.int32, device=self.device))
+
+    def affine_me(self, ref, cur, lam: float, align: int, ncp: int, extra: int = 0,
+                  prev: torch.Tensor | None = None, out=None):
+        ref, cur = self._frame(ref), self._frame(cur)
+        cost, cpmv = out if out is not None else self.alloc_result(align)
+        if ncp == 3 and (prev is None or prev.shape != (self.n_cus(align), 7)):
+            raise ValueError("3-CP needs prev = the same-alignment 2-CP cpmvs [n, 7]")
+        check(lib().vame_affine_me(self._h, _ptr(ref), _ptr(cur), float(lam), align, ncp, extra,
+                                   _ptr(prev.contiguous()) if prev is not None else None,
+                                   _ptr(cost), _ptr(cpmv), self._stream()))
+        return cost, cpmv
+
+    def alloc_poc(self, nrefs: int, modes: int = 3):
+        res = {}
+        for r in range(nrefs):
+            for m, name in enumerate(MODES):
+                if (m & 1) and not (modes & 2):
+                    continue
+                res[(r, name)] = self.alloc_result(m >> 1)
+        return res
+
+    def affine_me_poc(self, cur, refs, lam: float, modes: int = 3, extra: int = 0, out=None):
+        """modes: 1 = 2-CP only, 3 = 2-CP then 3-CP.  Returns {(refIdx, MODE): (cost, cpmv)}."""
+        cur = self._frame(cur)
+        refs = [self._frame(r) for r in refs]
+        out = out if out is not None else self.alloc_poc(len(refs), modes)
+        pr = PocResult()
+        for (r, name), (cost, cpmv) in out.items():
+            m = MODES.index(name)
+            pr.cost[r][m] = cost.data_ptr()
+            pr.cpmvs[r][m] = cpmv.data_ptr()
+        ref_ptrs = (ctypes.c_void_p * len(refs))(*[r.data_ptr() for r in refs])
+        check(lib().vame_affine_me_poc(self._h, _ptr(cur), ref_ptrs, len(refs), float(lam), modes,
+                                       extra, ctypes.byref(pr), self._stream()))
+        return out
