@@ -17,9 +17,14 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
 LIB_SRCS := $(CSRC)/vame_engine.hip $(CSRC)/vame_hostlogic.cpp
 LIB_HDRS := $(CSRC)/vame_kernel.h $(CSRC)/vame_tables.h include/vame.h
 
-all: lib cli oracle
+all: lib oracle
 
 lib: $(LIBDIR)/libvame.so
+
+# timing-only ablation builds (results are wrong): make ablate
+ablate:
+	@mkdir -p $(LIBDIR)
+	for a in 1 2 4 6 7 8 11 13 14 15; do $(HIPCC) $(HIPFLAGS) -DVAME_ABLATE=$$a -shared -o $(LIBDIR)/libvame_ablate$$a.so $(LIB_SRCS) || exit 1; done
 cli: $(BINDIR)/vame
 
 $(LIBDIR)/libvame.so: $(LIB_SRCS) $(LIB_HDRS)

@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the affine-ME hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4] [--qp QP]
+
+One step = the hot path over one batch of synthetic input: every (POC, refIdx)
+pair of the configuration's frames (refs from the reference's 4-slot list,
+lambda from its GOP-8 model), FULL + HALF candidate CUs, 2-CP (and 3-CP where
+the config asks for it), inputs resident in HBM.  Default = BASELINE.json
+configs[1]: 1920x1080 QP32, 2 frames, 2-CPMV affine only (3 pairs, 196,425
+candidate CUs per step).  Multi-GPU (torchrun, one rank per GPU): every rank
+codes its own frame shard (weak scaling) and the per-rank decision results are
+gathered to every rank with one RCCL all_gather per step (the decision-log
+gather of SURVEY.md §8e).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "vvc-affine-gpu_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+CONFIGS = {
+    "c2": dict(W=1920, H=1080, qp=32, frames=2, modes=1,
+               label="1920x1080 QP32, 2 frames, 2-CPMV affine only (FULL+HALF CUs)"),
+    "c3": dict(W=1920, H=1080, qp=32, frames=30, modes=3,
+               label="1920x1080 QP32, 30 frames, 2- and 3-CPMV affine (FULL+HALF CUs)"),
+    "c4": dict(W=3840, H=2160, qp=32, frames=30, modes=3,
+               label="3840x2160, 30 frames, 2- and 3-CPMV affine (FULL+HALF CUs)"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--qp", type=int, default=None)
+    ap.add_argument("--frames", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    if args.qp is not None:
+        cfg["qp"] = args.qp
+    if args.frames is not None:
+        cfg["frames"] = args.frames
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from vame import synth
+    from vame.engine import Engine
+    from vame.hostlogic import lambda_for_poc, ref_list
+    from vame.metrics import pair_accounting
+
+    W, H, qp, nf, modes = cfg["W"], cfg["H"], cfg["qp"], cfg["frames"], cfg["modes"]
+    ncps = (2, 3) if modes & 2 else (2,)
+    # this rank's frame shard (weak scaling: every rank codes nf frames of its own)
+    t0 = time.time()
+    orig, recon = synth.synth_sequence(W, H, nf, qp, seed=0x5EED + 7919 * rank)
+    log(f"[rank {rank}] synthesized {nf} frames {W}x{H} in {time.time() - t0:.1f}s")
+    d_orig = [torch.from_numpy(orig[k].view(np.int16)).to(dev) for k in range(nf)]
+    d_recon = [torch.from_numpy(recon[k].view(np.int16)).to(dev) for k in range(nf)]
+    eng = Engine(W, H, dev.index)
+
+    plan = []  # (poc, refs, lambda, out buffers)
+    for poc in range(1, nf + 1):
+        refs = ref_list(poc)
+        plan.append((poc, refs, lambda_for_poc(qp, poc), eng.alloc_poc(len(refs), modes)))
+    n_pairs = sum(len(p[1]) for p in plan)
+    acc = pair_accounting(W, H, ncps)
+    rows_per_step = n_pairs * acc["rows"]
+
+    gather_src = gather_dst = None
+    if dist is not None:
+        nbytes = sum(c.numel() * 8 + p.numel() * 4 for pl in plan for (c, p) in pl[3].values())
+        gather_src = torch.empty(nbytes // 4, dtype=torch.int32, device=dev)
+        gather_dst = torch.empty(world * gather_src.numel(), dtype=torch.int32, device=dev)
+
+    def step():
+        for (poc, refs, lam, out) in plan:
+            eng.affine_me_poc(d_orig[poc - 1], [d_recon[r] for r in refs], lam, modes, 0, out=out)
+        if dist is not None:  # decision-log gather over RCCL/xGMI
+            ofs = 0
+            for (_, _, _, out) in plan:
+                for (c, p) in out.values():
+                    n = c.numel() * 2
+                    gather_src[ofs:ofs + n].copy_(c.view(torch.int32))
+                    ofs += n
+                    gather_src[ofs:ofs + p.numel()].copy_(p.view(-1))
+                    ofs += p.numel()
+            dist.all_gather_into_tensor(gather_dst, gather_src)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    eng.set_timing(True)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    quad_ms, quad_n = eng.get_timing(0)
+    big_ms, big_n = eng.get_timing(1)
+    eng.set_timing(False)
+    tmax = elapsed
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tmax = float(t.item())
+
+    value = rows_per_step * world * args.steps / tmax
+    # roofline of the dominant kernel (quadrant work items, affine_me_quad)
+    quad_bytes = acc["bytes_quad"] * n_pairs * args.steps
+    achieved = quad_bytes / (quad_ms * 1e-3) / 1e9 if quad_ms > 0 else 0.0
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", f"pmc_{args.config}.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get("quad_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": "candidate CU-blocks/s at 1080p QP32; bit-exact CPMV/cost match vs reference",
+        "value": value,
+        "unit": "CU-blocks/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": tmax * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {"workload": cfg["label"], "resolution": f"{W}x{H}", "qp": qp, "frames": nf,
+                   "pairs_per_step": n_pairs, "rows_per_step_per_gpu": rows_per_step,
+                   "modes": "2cp+3cp" if modes & 2 else "2cp", "parallelism": f"frame-shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "affine_me_quad",
+                     "avg_launch_ms": quad_ms / max(quad_n, 1),
+                     "alg_bytes_per_launch": quad_bytes / max(quad_n, 1),
+                     "big_kernel_avg_launch_ms": big_ms / max(big_n, 1)},
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"], result["parity_sample"] = cpu_baseline(
+            orig, recon, plan[0], acc, ncps, W, H, eng, modes)
+    if dist is not None:
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(orig, recon, plan0, acc, ncps, W, H, eng, modes):
+    """The CPU oracle (C restatement, OpenMP) on one pair of the workload, and a
+    bit-exact check of the GPU output for that pair against it."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_py as O
+    try:
+        threads = min(16, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        threads = min(16, os.cpu_count() or 1)
+    poc, refs, lam, out = plan0
+    ref, cur = recon[refs[0]], orig[poc - 1]
+    t0 = time.perf_counter()
+    res = O.affine_me_pair(ref, cur, lam, 0, modes=ncps, nthreads=threads)
+    dt = time.perf_counter() - t0
+    rows = acc["rows"]
+    ok = True
+    for name, key in (("FULL_2CP", (0, 2)), ("FULL_3CP", (0, 3)), ("HALF_2CP", (1, 2)),
+                      ("HALF_3CP", (1, 3))):
+        if key not in res:
+            continue
+        c, p = out[(0, name)]
+        oc, op = res[key]
+        gc = c.cpu().numpy()
+        gp = p.cpu().numpy()[:, 1:]
+        opp = np.stack([op[f] for f in ("LTx", "LTy", "RTx", "RTy", "LBx", "LBy")], 1)
+        ok &= bool((gc == oc).all() and (gp == opp).all())
+    base = {"value": rows / dt, "unit": "CU-blocks/s", "cores": threads, "kind": "port",
+            "sample": f"{W}x{H} POC{poc}/ref0 pair, FULL+HALF {'+'.join(f'{n}CP' for n in ncps)} "
+                      f"({rows} candidate CUs), oracle/vame_oracle.c OpenMP, {dt:.2f}s"}
+    return base, {"pair": f"POC{poc}/ref0", "rows": rows, "bit_exact": ok}
+
+
+if __name__ == "__main__":
+    main()

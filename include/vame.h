@@ -78,6 +78,15 @@ int vame_affine_me_poc(vame_ctx* ctx, const uint16_t* cur, const uint16_t* const
                        int nrefs, float lambda, int mode_mask, int extra_grad_iter,
                        const vame_poc_result* out, void* stream);
 
+/* Device-side kernel timing (the reference's per-PRED kernelExecutionTime,
+ * main.cpp:856-866): when enabled, every kernel launch is bracketed by hipEvents
+ * on the stream it runs on.  kernel_class 0 = quadrant work items
+ * (affine_me_quad), 1 = 128-class work items (affine_me_ctu).
+ * vame_get_timing waits for the recorded launches and returns their summed
+ * duration and count since the last reset. */
+int vame_set_timing(vame_ctx* ctx, int enable);
+int vame_get_timing(vame_ctx* ctx, int kernel_class, double* total_ms, int* launches, int reset);
+
 /* Geometry / host helpers (no device work). */
 int vame_num_ctus(int width, int height);   /* 0 if unsupported */
 int vame_cus_per_ctu(int align);            /* 201 / 284 */

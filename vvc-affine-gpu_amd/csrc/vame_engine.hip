@@ -40,6 +40,10 @@ struct vame_ctx {
   int nQuadFull = 0, nQuadHalf = 0, nBig = 0;
   hipStream_t side = nullptr;   // second stream: 128-class items run beside the quadrant items
   hipEvent_t evFork = nullptr, evJoin = nullptr;
+  // optional per-kernel timing: (start, end) event pairs per kernel class
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];
+  size_t evUsed[2] = {0, 0};
 };
 
 namespace {
@@ -149,7 +153,33 @@ void fill_common(KParams& kp, const vame_ctx* c, float lambda, int extra) {
   kp.extra = extra;
 }
 
-int launch(const vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
+// timing hooks (no-ops unless vame_set_timing(ctx, 1))
+int time_begin(vame_ctx* c, int cls, hipStream_t s) {
+  if (!c->timing) return VAME_OK;
+  auto& v = c->ev[cls];
+  if (c->evUsed[cls] == v.size()) {
+    std::pair<hipEvent_t, hipEvent_t> e;
+    VAME_HIP(hipEventCreate(&e.first));
+    VAME_HIP(hipEventCreate(&e.second));
+    v.push_back(e);
+  }
+  VAME_HIP(hipEventRecord(v[c->evUsed[cls]].first, s));
+  return VAME_OK;
+}
+int time_end(vame_ctx* c, int cls, hipStream_t s) {
+  if (!c->timing) return VAME_OK;
+  VAME_HIP(hipEventRecord(c->ev[cls][c->evUsed[cls]].second, s));
+  c->evUsed[cls]++;
+  return VAME_OK;
+}
+
+#define VAME_TRY(x)        \
+  do {                     \
+    int rc_ = (x);         \
+    if (rc_) return rc_;   \
+  } while (0)
+
+int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
            hipStream_t stream) {
   // 128-class items (big LDS, 1 workgroup per CU) go first on a side stream so
   // they overlap with the quadrant items instead of forming a tail.
@@ -165,8 +195,10 @@ int launch(const vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool big
       VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
       s = c->side;
     }
-    hipLaunchKernelGGL(affine_me_kernel<128>, dim3(grid), dim3(kThreads), 0, s, kb);
+    VAME_TRY(time_begin(c, 1, s));
+    hipLaunchKernelGGL(affine_me_ctu, dim3(grid), dim3(kThreads), 0, s, kb);
     VAME_HIP(hipGetLastError());
+    VAME_TRY(time_end(c, 1, s));
     if (fork) VAME_HIP(hipEventRecord(c->evJoin, s));
   }
   if (quadFull || quadHalf) {
@@ -174,8 +206,10 @@ int launch(const vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool big
     kq.items = quadFull ? c->dQuad : c->dQuad + c->nQuadFull;
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
     const unsigned grid = (unsigned)(kq.nItems * kq.nCtus * kq.nRefs);
-    hipLaunchKernelGGL(affine_me_kernel<64>, dim3(grid), dim3(kThreads), 0, stream, kq);
+    VAME_TRY(time_begin(c, 0, stream));
+    hipLaunchKernelGGL(affine_me_quad, dim3(grid), dim3(kThreads), 0, stream, kq);
     VAME_HIP(hipGetLastError());
+    VAME_TRY(time_end(c, 0, stream));
   }
   if (fork) VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
   return VAME_OK;
@@ -264,6 +298,11 @@ void vame_destroy(vame_ctx* c) {
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->evFork) (void)hipEventDestroy(c->evFork);
   if (c->evJoin) (void)hipEventDestroy(c->evJoin);
+  for (int k = 0; k < 2; k++)
+    for (auto& e : c->ev[k]) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
   delete c;
 }
 
@@ -322,6 +361,29 @@ int vame_affine_me_poc(vame_ctx* c, const uint16_t* cur, const uint16_t* const* 
     }
   }
   return launch(c, kp, true, true, true, (hipStream_t)stream);
+}
+
+int vame_set_timing(vame_ctx* c, int enable) {
+  if (!c) return VAME_E_INVALID;
+  c->timing = enable != 0;
+  c->evUsed[0] = c->evUsed[1] = 0;
+  return VAME_OK;
+}
+
+int vame_get_timing(vame_ctx* c, int cls, double* total_ms, int* launches, int reset) {
+  if (!c || cls < 0 || cls > 1 || !total_ms || !launches) return VAME_E_INVALID;
+  VAME_HIP(hipSetDevice(c->device));
+  double t = 0;
+  for (size_t i = 0; i < c->evUsed[cls]; i++) {
+    float ms = 0;
+    VAME_HIP(hipEventSynchronize(c->ev[cls][i].second));
+    VAME_HIP(hipEventElapsedTime(&ms, c->ev[cls][i].first, c->ev[cls][i].second));
+    t += ms;
+  }
+  *total_ms = t;
+  *launches = (int)c->evUsed[cls];
+  if (reset) c->evUsed[cls] = 0;
+  return VAME_OK;
 }
 
 const char* vame_strerror(int code) {

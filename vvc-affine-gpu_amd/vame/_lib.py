@@ -12,7 +12,8 @@ LIB_PATH = os.environ.get("VAME_LIB", os.path.join(PKG_DIR, "lib", "libvame.so")
 EXPORTS = (
     "vame_create", "vame_destroy", "vame_affine_me", "vame_affine_me_poc", "vame_num_ctus",
     "vame_cus_per_ctu", "vame_num_groups", "vame_group_geometry", "vame_lambda", "vame_poc_qp",
-    "vame_ref_list", "vame_strerror", "vame_last_hip_error", "vame_version",
+    "vame_ref_list", "vame_strerror", "vame_last_hip_error", "vame_version", "vame_set_timing",
+    "vame_get_timing",
 )
 
 
@@ -51,6 +52,9 @@ def lib():
         L.vame_strerror.restype = ctypes.c_char_p
         L.vame_last_hip_error.restype = ctypes.c_char_p
         L.vame_version.restype = ctypes.c_char_p
+        L.vame_set_timing.argtypes = [P, I]
+        L.vame_get_timing.argtypes = [P, I, ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_int), I]
         _lib = L
     return _lib
 

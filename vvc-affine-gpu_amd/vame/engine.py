@@ -49,6 +49,15 @@ class Engine:
         except Exception:
             pass
 
+    def set_timing(self, enable: bool) -> None:
+        check(lib().vame_set_timing(self._h, int(enable)))
+
+    def get_timing(self, kernel_class: int, reset: bool = True):
+        """(total_ms, launches) of kernel class 0 (quadrant items) / 1 (128-class items)."""
+        t, n = ctypes.c_double(), ctypes.c_int()
+        check(lib().vame_get_timing(self._h, kernel_class, ctypes.byref(t), ctypes.byref(n), int(reset)))
+        return t.value, n.value
+
     def n_cus(self, align: int) -> int:
         return self.n_ctus * (284 if align else 201)
 
