@@ -58,18 +58,55 @@ struct CuDesc {
   int x, y, w, h, align, outOff;
 };
 
-Item make_item(int rx, int ry, std::vector<CuDesc> cus) {
-  // larger CUs first: every CU's first lane is then aligned to its own
-  // (power-of-two) lane count, which the segmented wave reductions rely on
+// One work item.  sbpl = sub-blocks per lane of the kernel class (1 quadrant,
+// 4 CTU).  Quadrant items whose CUs all fit one wave (<= 64 sub-blocks) are
+// "autonomous": CUs are first-fit packed into <= 4 waves of 64 lanes and every
+// wave refines its own CUs; other items are "cooperative" (CUs span waves,
+// workgroup barriers per phase).  In both modes larger CUs come first inside
+// their lane range, so every CU's first lane is aligned to its own
+// power-of-two lane count, which the segmented wave reductions rely on.
+Item make_item(int rx, int ry, std::vector<CuDesc> cus, int sbpl) {
   std::stable_sort(cus.begin(), cus.end(),
                    [](const CuDesc& a, const CuDesc& b) { return a.w * a.h > b.w * b.h; });
+  if ((int)cus.size() > kMaxCu) abort();
   Item it;
   memset(&it, 0, sizeof(it));
-  if ((int)cus.size() > kMaxCu) abort();
   it.nCu = (int16_t)cus.size();
   it.rx = (int16_t)rx;
   it.ry = (int16_t)ry;
-  int sb = 0;
+  bool coop = sbpl > 1;
+  for (auto& c : cus) coop |= c.w * c.h / 16 > 64;
+  std::vector<int> waveOf(cus.size(), 0);
+  int nWaves = 1;
+  if (!coop) {
+    int fill[kMaxWaves] = {0, 0, 0, 0};
+    nWaves = 0;
+    for (size_t k = 0; k < cus.size(); k++) {
+      const int nsb = cus[k].w * cus[k].h / 16;
+      int w = 0;
+      while (w < nWaves && fill[w] + nsb > 64) w++;
+      if (w == nWaves) nWaves++;
+      if (nWaves > kMaxWaves) abort();
+      fill[w] += nsb;
+      waveOf[k] = w;
+    }
+    // CU slots grouped by wave (stable: still largest first inside a wave)
+    std::vector<size_t> order(cus.size());
+    for (size_t k = 0; k < order.size(); k++) order[k] = k;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](size_t a, size_t b) { return waveOf[a] < waveOf[b]; });
+    std::vector<CuDesc> c2;
+    std::vector<int> w2;
+    for (size_t k : order) {
+      c2.push_back(cus[k]);
+      w2.push_back(waveOf[k]);
+    }
+    cus.swap(c2);
+    waveOf.swap(w2);
+  }
+  it.coop = coop ? 1 : 0;
+  it.nWaves = (int16_t)(coop ? kMaxWaves : nWaves);
+  int sb = 0, waveSb0 = 0, prevWave = -1;
   for (size_t k = 0; k < cus.size(); k++) {
     CuSlot& s = it.cu[k];
     s.x = (int16_t)cus[k].x;
@@ -79,9 +116,23 @@ Item make_item(int rx, int ry, std::vector<CuDesc> cus) {
     s.align = (uint8_t)cus[k].align;
     s.outOff = (int16_t)cus[k].outOff;
     s.sbBase = (int16_t)sb;
+    if (coop) {
+      s.laneBase = (int16_t)(sb / sbpl);
+    } else {
+      const int w = waveOf[k];
+      if (w != prevWave) {
+        it.wave[w].cuBegin = (int16_t)k;
+        waveSb0 = sb;
+        prevWave = w;
+      }
+      it.wave[w].cuEnd = (int16_t)(k + 1);
+      it.wave[w].nSb = (int16_t)(sb + cus[k].w * cus[k].h / 16 - waveSb0);
+      s.laneBase = (int16_t)(sb - waveSb0);
+    }
     sb += cus[k].w * cus[k].h / 16;
   }
   it.nSb = (int16_t)sb;
+  if (sb > kThreads * sbpl) abort();
   return it;
 }
 
@@ -96,7 +147,7 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& quadFull,
     if (w == 128 || h == 128) {
       std::vector<CuDesc> c;
       for (int k = 0; k < n; k++) c.push_back({(k % cols) * w, (k / cols) * h, w, h, 0, kFullStride[g] + k});
-      big.push_back(make_item(0, 0, c));
+      big.push_back(make_item(0, 0, c, Cfg<128>::SBPL));
       continue;
     }
     for (int q = 0; q < 4; q++) {
@@ -106,7 +157,7 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& quadFull,
         const int x = (k % cols) * w, y = (k / cols) * h;
         if (x >= qx && x < qx + 64 && y >= qy && y < qy + 64) c.push_back({x, y, w, h, 0, kFullStride[g] + k});
       }
-      quadFull.push_back(make_item(qx, qy, c));
+      quadFull.push_back(make_item(qx, qy, c, Cfg<64>::SBPL));
     }
   }
   for (int q = 0; q < 4; q++) {
@@ -140,7 +191,7 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& quadFull,
         }
       if (!placed) bins.push_back({gr.sbTotal, gr.cus});
     }
-    for (auto& bn : bins) quadHalf.push_back(make_item(qx, qy, bn.second));
+    for (auto& bn : bins) quadHalf.push_back(make_item(qx, qy, bn.second, Cfg<64>::SBPL));
   }
 }
 

@@ -1,21 +1,31 @@
 // vame_kernel.h -- HIP/CDNA4 device code of the affine-ME hot path.
 //
-// One workgroup (256 threads) = one work item: a 64x64 quadrant (or, for the
-// 128-wide/high aligned sizes, the whole 128x128 CTU) of one CTU, for one
-// reference frame, holding the candidate CUs of one or more CU-size groups.
-// The workgroup runs the complete gradient-based CPMV refinement of
-// affine.cl:195-917 for all of them -- 2 control points, then 3 control
-// points seeded from the 2-CP winner of the same CU (affine.cl:81-105) --
-// without leaving the CU:
-//   * the reference frame region (+16 px margin, clamp-to-edge padded) is
-//     staged once into LDS; every 9x9 filter window of every iteration is read
-//     from there (windows outside the tile fall back to clamped global loads);
-//   * predictions live in a per-CU-compact LDS buffer; gradients are computed
-//     on the fly from it (no global gradient / equation scratch);
-//   * the normal equations are reduced as 24 exact integer moments per CU
-//     (wave butterflies + LDS int64 atomics) and solved by one lane per CU
-//     with the reference's double-precision elimination, operation for
-//     operation.
+// One workgroup (256 threads = 4 waves) = one work item: a 64x64 quadrant of a
+// CTU (kernel affine_me_quad) or, for the 128-wide/high aligned sizes, the
+// whole 128x128 CTU (kernel affine_me_ctu), for one reference frame, holding
+// the candidate CUs of one or more CU-size groups.  The workgroup runs the
+// complete gradient-based CPMV refinement of affine.cl:195-917 for all of them
+// -- 2 control points, then 3 control points seeded from the 2-CP winner of
+// the same CU (affine.cl:81-105) -- without leaving the CU:
+//   * the reference region (+16 px margin, clamp-to-edge padded) is staged
+//     once into LDS; every 9x9 filter window of every iteration is read from
+//     there (windows leaving the tile fall back to clamped global loads);
+//   * predictions live in a CU-compact LDS buffer; gradients are computed on
+//     the fly from it (no global gradient / equation scratch);
+//   * each CU's normal equations are reduced as exact integer sums (14 values
+//     for 2 CP, 24 moments for 3 CP) with DPP segment reductions and solved by
+//     one lane per CU with the reference's double-precision elimination,
+//     operation for operation, in registers.
+// Two scheduling modes per work item (chosen on the host, vame_engine.hip):
+//   autonomous  every CU has <= 64 sub-blocks and is owned by ONE wave; each
+//               wave iterates its CUs on its own (wave-local LDS ordering
+//               only, no workgroup barrier inside the iteration loop);
+//   cooperative larger CUs span several waves; one workgroup barrier per phase
+//               and the partial sums meet in LDS int64 atomics.
+// Per iteration and CU: predict (one lane per 4x4 sub-block: MV field, window,
+// 6-tap H/V filter on v_dot2_i32_i16, SATD) -> cost (one lane per CU) ->
+// gradient (Sobel on packed int16 sample pairs, CU-border replication,
+// residual, five dot2 sums per sub-block) -> solve (one lane per CU).
 // Bit-exactness notes (SURVEY.md §8a traps): integer math is exact and
 // order-free; the only float work is floor(lambda*bits) (single precision)
 // and the FP64 solve (compiled with -ffp-contract=off, explicit fma where the
@@ -28,10 +38,13 @@
 
 namespace vame {
 
-constexpr int kMaxCu = 32;   // CU slots per work item
-constexpr int kMargin = 16;  // LDS reference-tile margin around the work-item region
+constexpr int kMaxCu = 32;    // CU slots per work item
+constexpr int kMaxWaves = 4;
+constexpr int kMargin = 16;   // LDS reference-tile margin around the work-item region
 constexpr int kThreads = 256;
-constexpr int kNumMom = 24;  // {1,u,v,uu,uv,vv} x {xx,xy,yy} + {1,u,v} x {xe,ye}
+constexpr int kNumMom = 24;   // 3 CP: {1,u,v,uu,uv,vv} x {xx,xy,yy} + {1,u,v} x {xe,ye}
+constexpr int kNumVal2 = 14;  // 2 CP: 10 distinct matrix entries + 4 right-hand sides
+constexpr int kPredPad = 8;   // samples in front of the LDS prediction buffer
 
 // device view of vame_cpmvs / typedef.h Cpmvs (28 bytes)
 struct vame_cpmvs_dev {
@@ -44,13 +57,22 @@ struct CuSlot {     // 16 bytes
   uint8_t align;    // 0 FULL, 1 HALF
   uint8_t pad0;
   int16_t outOff;   // RETURN_STRIDE[group] + cuIdx
-  int16_t sbBase;   // first sub-block (lane-major) of this CU inside the item
-  int32_t pad1;
+  int16_t sbBase;   // first sub-block of this CU inside the item (prediction buffer / 16)
+  int16_t laneBase; // first lane of this CU (wave lane when autonomous, thread when cooperative)
+  int16_t pad1;
+};
+
+struct WaveDesc {   // 8 bytes: the CU slots a wave owns (autonomous items)
+  int16_t cuBegin, cuEnd, nSb, pad;
 };
 
 struct Item {
-  int16_t nCu, nSb;  // CU slots, sub-blocks
-  int16_t rx, ry;    // region origin (CTU-relative)
+  int16_t nCu, nSb;   // CU slots, sub-blocks
+  int16_t rx, ry;     // region origin (CTU-relative)
+  int16_t nWaves;     // waves holding CUs
+  int16_t coop;       // 1: cooperative mode
+  int16_t pad0, pad1;
+  WaveDesc wave[kMaxWaves];
   CuSlot cu[kMaxCu];
 };
 
@@ -68,9 +90,41 @@ struct KParams {
   int run2, run3;
 };
 
+// VAME_ABLATE (timing-only builds, results are wrong): bit 0 skip the solve,
+// bit 1 skip the gradient math, bit 2 skip the reductions of the equations,
+// bit 3 skip the prediction math.
+#ifndef VAME_ABLATE
+#define VAME_ABLATE 0
+#endif
+
 // ------------------------------------------------------------------ helpers
+typedef short short2v __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
 __device__ __forceinline__ int shl(int a, int s) { return (int)((unsigned)a << s); }
+__device__ __forceinline__ short2v as_s2(unsigned v) { return __builtin_bit_cast(short2v, v); }
+__device__ __forceinline__ unsigned as_u(short2v v) { return __builtin_bit_cast(unsigned, v); }
+// v_dot2_i32_i16: a.lo*b.lo + a.hi*b.hi + acc (signed 16-bit halves, no clamp)
+__device__ __forceinline__ int dot2(unsigned a, unsigned b, int acc) {
+  return __builtin_amdgcn_sdot2(as_s2(a), as_s2(b), acc, false);
+}
+// low 16 bits of lo | low 16 bits of hi << 16
+__device__ __forceinline__ unsigned pack16(int lo, int hi) {
+  return __builtin_amdgcn_perm((unsigned)hi, (unsigned)lo, 0x05040100u);
+}
+
+// LDS ordering between the lanes of one wave (a wave's LDS ops execute in order)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void phase_sync(bool coop) {
+  if (coop)
+    __syncthreads();
+  else
+    wave_sync();
+}
 
 // aux_functions.cl:51-67 clipMv
 __device__ __forceinline__ void clip_mv(int& x, int& y, int bx, int by, int W, int H) {
@@ -157,7 +211,7 @@ __device__ __forceinline__ int seg_sum32(int v, int S, int smax) {
   if (smax > 32) { int o = __shfl_down(v, 32); if (S > 32) v += o; }
   return v;
 }
-// wave-uniform maximum of a small positive per-lane value
+// wave-uniform maximum of a small positive per-lane power of two
 __device__ __forceinline__ int wave_max_pow2(int S) {
   int m = 1;
   if (__any(S > 1)) m = 2;
@@ -169,105 +223,345 @@ __device__ __forceinline__ int wave_max_pow2(int S) {
   return m;
 }
 
-__device__ __forceinline__ void luma_coeffs(int frac, int* c) {
-#pragma unroll
-  for (int m = 0; m < 6; m++) c[m] = kLuma6[frac][m];
+// ---------------------------------------------------------- filter tap pairs
+// kLuma6 (constants.cl:40-58) re-packed for v_dot2_i32_i16.  A 4-wide output
+// row reads 5 dwords D[0..4] of its window row (two samples each); output c
+// applies set s' + (c & 1) to D[(c >> 1) .. (c >> 1) + 3], where s' is the
+// parity of the window start inside the dword stream:
+//   set 0: (f0,f1) (f2,f3) (f4,f5) (0,0)     set 1: (0,f0) (f1,f2) (f3,f4) (f5,0)
+//   set 2: (0,0) (f0,f1) (f2,f3) (f4,f5)
+// The vertical pass uses sets 0/1 on row pairs (t[2k], t[2k+1]) the same way.
+struct CoefTab {
+  uint32_t v[16][3][4];
+};
+constexpr uint32_t pk16c(int lo, int hi) {
+  return (uint32_t)(uint16_t)(int16_t)lo | ((uint32_t)(uint16_t)(int16_t)hi << 16);
 }
-
-// Linear forms of the equation regressors in (1, u, v): iC_c = alpha_c . gx + beta_c . gy
-// 2 CP (affine.cl:691-694): gx, u gx + v gy, gy, v gx - u gy
-// 3 CP (affine.cl:684-689): gx, u gx, gy, u gy, v gx, v gy
-__constant__ int8_t kAlpha2[4][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 0}, {0, 0, 1}};
-__constant__ int8_t kBeta2[4][3] = {{0, 0, 0}, {0, 0, 1}, {1, 0, 0}, {0, -1, 0}};
-__constant__ int8_t kAlpha3[6][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1}, {0, 0, 0}};
-__constant__ int8_t kBeta3[6][3] = {{0, 0, 0}, {0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 0}, {0, 0, 1}};
-
-// product of two linear forms in (1,u,v) -> moment index {1,u,v,uu,uv,vv} weighted sum
-__device__ __forceinline__ long long quad_form(const int8_t* p, const int8_t* q, const long long* m) {
-  long long r = 0;
-  r += (long long)(p[0] * q[0]) * m[0];
-  r += (long long)(p[0] * q[1] + p[1] * q[0]) * m[1];
-  r += (long long)(p[0] * q[2] + p[2] * q[0]) * m[2];
-  r += (long long)(p[1] * q[1]) * m[3];
-  r += (long long)(p[1] * q[2] + p[2] * q[1]) * m[4];
-  r += (long long)(p[2] * q[2]) * m[5];
-  return r;
-}
-
-
-// One CU's normal equations solved by an 8-lane group (lane j holds row j+1 of
-// the reference's private_dEqualCoeff, affine.cl:759-763), reproducing VTM
-// solveEqual (affine.cl:782-856) operation for operation:
-//   pivot search with the sequential strict-'>' scan (NaN never wins),
-//   row swap, elimination a[j][k] -= a[i][k]*a[j][i-1]/a[i][i-1] (no zero-pivot
-//   guard), back-substitution with fma (FP_CONTRACT) and the zero-pivot reset.
-// Must be called by every lane of the wave (shuffles); `act` marks lanes whose
-// group holds a live CU.  Returns the affine parameters in p on every lane.
-template <int NCP>
-__device__ __forceinline__ void group_solve(const long long* __restrict__ M, bool act, int lane,
-                                            double (&p)[2 * NCP]) {
-  constexpr int N = 2 * NCP;
-  const int j = lane & 7, base = lane & ~7;
-  const int jr = j < N ? j : N - 1;
-  double a[N + 1];
-  {
-    const int8_t* al = NCP == 3 ? kAlpha3[jr] : kAlpha2[jr];
-    const int8_t* be = NCP == 3 ? kBeta3[jr] : kBeta2[jr];
-#pragma unroll
-    for (int r = 0; r < N; r++) {
-      const int8_t* al2 = NCP == 3 ? kAlpha3[r] : kAlpha2[r];
-      const int8_t* be2 = NCP == 3 ? kBeta3[r] : kBeta2[r];
-      long long A = quad_form(al, al2, M + 0) + quad_form(al, be2, M + 6) +
-                    quad_form(be, al2, M + 6) + quad_form(be, be2, M + 12);
-      a[r] = (act && j < N) ? (double)A : 0.0;
+constexpr CoefTab make_coef_tab() {
+  CoefTab t{};
+  for (int f = 0; f < 16; f++) {
+    const int8_t* c = kLuma6[f];
+    const uint32_t s0[4] = {pk16c(c[0], c[1]), pk16c(c[2], c[3]), pk16c(c[4], c[5]), 0u};
+    const uint32_t s1[4] = {pk16c(0, c[0]), pk16c(c[1], c[2]), pk16c(c[3], c[4]), pk16c(c[5], 0)};
+    const uint32_t s2[4] = {0u, pk16c(c[0], c[1]), pk16c(c[2], c[3]), pk16c(c[4], c[5])};
+    for (int k = 0; k < 4; k++) {
+      t.v[f][0][k] = s0[k];
+      t.v[f][1][k] = s1[k];
+      t.v[f][2][k] = s2[k];
     }
-    long long bsum = 0;
-#pragma unroll
-    for (int k = 0; k < 3; k++) bsum += (long long)al[k] * M[18 + k] + (long long)be[k] * M[21 + k];
-    a[N] = (act && j < N) ? (double)(bsum * 8) : 0.0;
   }
-  const int myRow = j + 1;
+  return t;
+}
+__constant__ CoefTab kCoefTab = make_coef_tab();
+
+// ------------------------------------------------------------- motion field
+struct MvField {
+  int bx, by, hx, hy, vx, vy;
+  bool spread;
+};
+
+// deriveMv{2,3}Cps_and_spread (aux_functions.cl:146-212), once per CU and iteration
+__device__ __forceinline__ MvField mv_field(const int* cp, int ncp, int lw, int lh) {
+  MvField f;
+  f.hx = shl(cp[2] - cp[0], 7 - lw);
+  f.hy = shl(cp[3] - cp[1], 7 - lw);
+  if (ncp == 3) {
+    f.vx = shl(cp[4] - cp[0], 7 - lh);
+    f.vy = shl(cp[5] - cp[1], 7 - lh);
+  } else {
+    f.vx = -f.hy;
+    f.vy = f.hx;
+  }
+  f.spread = spread_over_limit(f.hx, f.hy, f.vx, f.vy);
+  f.bx = shl(cp[0], 7);
+  f.by = shl(cp[1], 7);
+  return f;
+}
+
+struct Geo {       // a lane's CU
+  int x, y;        // frame position
+  int lw, lh, w, h;
+  int predBase;    // first sample of the CU in the LDS prediction buffer
+};
+
+// One 4x4 sub-block: affine MV (affine.cl:215-252), 9x9 window with
+// clamp-to-edge (affine.cl:254-326), separable 6-tap filter (aux_functions.cl
+// :1096-1239, PROF off), prediction to LDS, SATD against the original
+// (aux_functions.cl:1940-2043).
+template <int TILE, int TP>
+__device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, const Geo& g,
+                                          const uint16_t* s_tile, int tx0, int ty0,
+                                          const uint16_t* __restrict__ ref,
+                                          const uint16_t* __restrict__ cur, int W, int H,
+                                          uint16_t* s_pred, const uint4* s_coef) {
+  const int px = f.spread ? (g.w >> 1) : sx + 2, py = f.spread ? (g.h >> 1) : sy + 2;
+  int mx = f.bx + f.hx * px + f.vx * py, my = f.by + f.hy * px + f.vy * py;
+  mx = (mx + 64 - (mx >= 0)) >> 7;  // roundMv (aux_functions.cl:38-47)
+  my = (my + 64 - (my >= 0)) >> 7;
+  clip_mv(mx, my, g.x, g.y, W, H);
+  const int ix = mx >> 4, fx = mx & 15, iy = my >> 4, fy = my & 15;
+  const int wx = g.x + sx + ix - 2, wy = g.y + sy + iy - 2;  // window origin (frame)
+  const int tx = wx - tx0, ty = wy - ty0;
+  const bool inTile = (unsigned)tx <= (unsigned)(TILE - 9) && (unsigned)ty <= (unsigned)(TILE - 9);
+  const int sp = inTile ? (tx & 1) : 0;
+  const uint4 KA = s_coef[fx * 3 + sp], KB = s_coef[fx * 3 + sp + 1];
+  const uint4 G0 = s_coef[fy * 3 + 0], G1 = s_coef[fy * 3 + 1];
+  int tr[9][4];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    unsigned D[5];
+    if (inTile) {
+      const unsigned* src = reinterpret_cast<const unsigned*>(s_tile) + (((ty + i) * TP + tx) >> 1);
+#pragma unroll
+      for (int k = 0; k < 5; k++) D[k] = src[k];
+    } else {
+      const uint16_t* row = ref + (size_t)clampi(wy + i, 0, H - 1) * W;
+      unsigned w9[10];
+#pragma unroll
+      for (int m = 0; m < 9; m++) w9[m] = row[clampi(wx + m, 0, W - 1)];
+      w9[9] = 0;
+#pragma unroll
+      for (int k = 0; k < 5; k++) D[k] = w9[2 * k] | (w9[2 * k + 1] << 16);
+    }
+    // offset -IF_INTERNAL_OFFS << 2 = -32768, shift 2 (aux_functions.cl:1128-1161)
+    tr[i][0] = dot2(D[0], KA.x, dot2(D[1], KA.y, dot2(D[2], KA.z, dot2(D[3], KA.w, -32768)))) >> 2;
+    tr[i][1] = dot2(D[0], KB.x, dot2(D[1], KB.y, dot2(D[2], KB.z, dot2(D[3], KB.w, -32768)))) >> 2;
+    tr[i][2] = dot2(D[1], KA.x, dot2(D[2], KA.y, dot2(D[3], KA.z, dot2(D[4], KA.w, -32768)))) >> 2;
+    tr[i][3] = dot2(D[1], KB.x, dot2(D[2], KB.y, dot2(D[3], KB.z, dot2(D[4], KB.w, -32768)))) >> 2;
+  }
+  // vertical: rows packed in pairs (t[2k], t[2k+1]); offset (1<<9) + (8192<<6),
+  // shift 10, clipPel to [0, 1023] (aux_functions.cl:1182-1223)
+  int pr[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    unsigned P[5];
+#pragma unroll
+    for (int k = 0; k < 4; k++) P[k] = pack16(tr[2 * k][c], tr[2 * k + 1][c]);
+    P[4] = pack16(tr[8][c], 0);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint4 G = (r & 1) ? G1 : G0;
+      const int b = r >> 1;
+      const int acc =
+          dot2(P[b], G.x, dot2(P[b + 1], G.y, dot2(P[b + 2], G.z, dot2(P[b + 3], G.w, 524800))));
+      pr[r][c] = clampi(acc >> 10, 0, 1023);
+    }
+  }
+  int diff[16];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    uint2 pk;
+    pk.x = pack16(pr[r][0], pr[r][1]);
+    pk.y = pack16(pr[r][2], pr[r][3]);
+    *reinterpret_cast<uint2*>(&s_pred[g.predBase + (sy + r) * g.w + sx]) = pk;
+    const uint2 o = *reinterpret_cast<const uint2*>(cur + (size_t)(g.y + sy + r) * W + g.x + sx);
+    diff[r * 4 + 0] = (int)(o.x & 0xFFFF) - pr[r][0];
+    diff[r * 4 + 1] = (int)(o.x >> 16) - pr[r][1];
+    diff[r * 4 + 2] = (int)(o.y & 0xFFFF) - pr[r][2];
+    diff[r * 4 + 3] = (int)(o.y >> 16) - pr[r][3];
+  }
+  // xCalcHADs4x4 (aux_functions.cl:1940-2043, JVET_R0164 DC weighting)
+  int m[16], d[16];
+  m[0] = diff[0] + diff[12]; m[1] = diff[1] + diff[13];
+  m[2] = diff[2] + diff[14]; m[3] = diff[3] + diff[15];
+  m[4] = diff[4] + diff[8];  m[5] = diff[5] + diff[9];
+  m[6] = diff[6] + diff[10]; m[7] = diff[7] + diff[11];
+  m[8] = diff[4] - diff[8];  m[9] = diff[5] - diff[9];
+  m[10] = diff[6] - diff[10]; m[11] = diff[7] - diff[11];
+  m[12] = diff[0] - diff[12]; m[13] = diff[1] - diff[13];
+  m[14] = diff[2] - diff[14]; m[15] = diff[3] - diff[15];
+  d[0] = m[0] + m[4];  d[1] = m[1] + m[5];  d[2] = m[2] + m[6];  d[3] = m[3] + m[7];
+  d[4] = m[8] + m[12]; d[5] = m[9] + m[13]; d[6] = m[10] + m[14]; d[7] = m[11] + m[15];
+  d[8] = m[0] - m[4];  d[9] = m[1] - m[5];  d[10] = m[2] - m[6]; d[11] = m[3] - m[7];
+  d[12] = m[12] - m[8]; d[13] = m[13] - m[9]; d[14] = m[14] - m[10]; d[15] = m[15] - m[11];
+  m[0] = d[0] + d[3];  m[1] = d[1] + d[2];  m[2] = d[1] - d[2];  m[3] = d[0] - d[3];
+  m[4] = d[4] + d[7];  m[5] = d[5] + d[6];  m[6] = d[5] - d[6];  m[7] = d[4] - d[7];
+  m[8] = d[8] + d[11]; m[9] = d[9] + d[10]; m[10] = d[9] - d[10]; m[11] = d[8] - d[11];
+  m[12] = d[12] + d[15]; m[13] = d[13] + d[14]; m[14] = d[13] - d[14]; m[15] = d[12] - d[15];
+  d[0] = m[0] + m[1];  d[1] = m[0] - m[1];  d[2] = m[2] + m[3];  d[3] = m[3] - m[2];
+  d[4] = m[4] + m[5];  d[5] = m[4] - m[5];  d[6] = m[6] + m[7];  d[7] = m[7] - m[6];
+  d[8] = m[8] + m[9];  d[9] = m[8] - m[9];  d[10] = m[10] + m[11]; d[11] = m[11] - m[10];
+  d[12] = m[12] + m[13]; d[13] = m[12] - m[13]; d[14] = m[14] + m[15]; d[15] = m[15] - m[14];
+  int sa = 0;
+#pragma unroll
+  for (int k = 1; k < 16; k++) sa += abs(d[k]);
+  sa += abs(d[0]) >> 2;
+  return (sa + 1) >> 1;
+}
+
+// One 4x4 sub-block of the gradient step (affine.cl:477-708): 3x3 Sobel on the
+// LDS prediction with the CU-border replication of affine.cl:506-540 (rows
+// first, then columns), residual orig - pred (affine.cl:547-579) and the five
+// sums S = (gx.gx, gx.gy, gy.gy, gx.e, gy.e).  Samples are handled as packed
+// int16 pairs: |g| <= 4092 and |e| <= 1023 fit, and v_dot2_i32_i16 sums stay
+// below 2^28 (exact).
+__device__ __forceinline__ void grad_sb(int sx, int sy, const Geo& g,
+                                        const uint16_t* __restrict__ cur, int W,
+                                        const uint16_t* s_pred, int S[5]) {
+  short2v O[6][3], E[6][2];
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    // prediction row clamped into the CU; dwords cover samples sx-2 .. sx+5.
+    // Samples outside the CU only reach gradients the replication overwrites.
+    const int rr = clampi(sy - 1 + i, 0, g.h - 1);
+    const unsigned* src =
+        reinterpret_cast<const unsigned*>(s_pred) + ((g.predBase + rr * g.w + sx - 2) >> 1);
+    const unsigned D0 = src[0], D1 = src[1], D2 = src[2], D3 = src[3];
+    O[i][0] = as_s2(__builtin_amdgcn_alignbit(D1, D0, 16));  // (sx-1, sx)
+    O[i][1] = as_s2(__builtin_amdgcn_alignbit(D2, D1, 16));  // (sx+1, sx+2)
+    O[i][2] = as_s2(__builtin_amdgcn_alignbit(D3, D2, 16));  // (sx+3, sx+4)
+    E[i][0] = as_s2(D1);                                     // (sx, sx+1)
+    E[i][1] = as_s2(D2);                                     // (sx+2, sx+3)
+  }
+  short2v gx[4][2], gy[4][2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    short2v Hd[6], Vs[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      Hd[i] = O[i][k + 1] - O[i][k];                      // p(c+1) - p(c-1)
+      Vs[i] = O[i][k] + E[i][k] + E[i][k] + O[i][k + 1];  // p(c-1) + 2 p(c) + p(c+1)
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      gx[r][k] = Hd[r] + Hd[r + 1] + Hd[r + 1] + Hd[r + 2];
+      gy[r][k] = Vs[r + 2] - Vs[r];
+    }
+  }
+  if (sy == 0) {
+#pragma unroll
+    for (int k = 0; k < 2; k++) { gx[0][k] = gx[1][k]; gy[0][k] = gy[1][k]; }
+  }
+  if (sy + 4 == g.h) {
+#pragma unroll
+    for (int k = 0; k < 2; k++) { gx[3][k] = gx[2][k]; gy[3][k] = gy[2][k]; }
+  }
+  if (sx == 0) {  // column 0 <- column 1: low half <- high half of pair 0
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      gx[r][0] = as_s2(__builtin_amdgcn_perm(as_u(gx[r][0]), as_u(gx[r][0]), 0x03020302u));
+      gy[r][0] = as_s2(__builtin_amdgcn_perm(as_u(gy[r][0]), as_u(gy[r][0]), 0x03020302u));
+    }
+  }
+  if (sx + 4 == g.w) {  // column 3 <- column 2: high half <- low half of pair 1
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      gx[r][1] = as_s2(__builtin_amdgcn_perm(as_u(gx[r][1]), as_u(gx[r][1]), 0x01000100u));
+      gy[r][1] = as_s2(__builtin_amdgcn_perm(as_u(gy[r][1]), as_u(gy[r][1]), 0x01000100u));
+    }
+  }
+  int sxx = 0, sxy = 0, syy = 0, sxe = 0, sye = 0;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint2 o = *reinterpret_cast<const uint2*>(cur + (size_t)(g.y + sy + r) * W + g.x + sx);
+    const unsigned e0 = as_u(as_s2(o.x) - E[r + 1][0]), e1 = as_u(as_s2(o.y) - E[r + 1][1]);
+    const unsigned x0 = as_u(gx[r][0]), x1 = as_u(gx[r][1]);
+    const unsigned y0 = as_u(gy[r][0]), y1 = as_u(gy[r][1]);
+    sxx = dot2(x0, x0, dot2(x1, x1, sxx));
+    sxy = dot2(x0, y0, dot2(x1, y1, sxy));
+    syy = dot2(y0, y0, dot2(y1, y1, syy));
+    sxe = dot2(x0, e0, dot2(x1, e1, sxe));
+    sye = dot2(y0, e0, dot2(y1, e1, sye));
+  }
+  S[0] = sxx; S[1] = sxy; S[2] = syy; S[3] = sxe; S[4] = sye;
+}
+
+// A sub-block's contribution to its CU's normal equations (affine.cl:683-707:
+// every sample of the sub-block uses the sub-block centre (u, v)).
+// 2 CP, iC = (gx, u gx + v gy, gy, v gx - u gy) (affine.cl:691-694): the 10
+// distinct entries of the symmetric matrix, then the 4 right-hand sides.
+__device__ __forceinline__ void values_2cp(const int S[5], long long u, long long v, long long* o) {
+  const long long xx = S[0], xy = S[1], yy = S[2], xe = S[3], ye = S[4];
+  const long long uu = u * u, uv = u * v, vv = v * v;
+  o[0] += xx;                                  // A00
+  o[1] += u * xx + v * xy;                     // A01
+  o[2] += xy;                                  // A02
+  o[3] += v * xx - u * xy;                     // A03
+  o[4] += uu * xx + 2 * uv * xy + vv * yy;     // A11
+  o[5] += u * xy + v * yy;                     // A12
+  o[6] += uv * xx + (vv - uu) * xy - uv * yy;  // A13
+  o[7] += yy;                                  // A22
+  o[8] += v * xy - u * yy;                     // A23
+  o[9] += vv * xx - 2 * uv * xy + uu * yy;     // A33
+  o[10] += xe;                                 // b0
+  o[11] += u * xe + v * ye;                    // b1
+  o[12] += ye;                                 // b2
+  o[13] += v * xe - u * ye;                    // b3
+}
+// 3 CP (affine.cl:684-689): moments {1,u,v,uu,uv,vv} x {xx,xy,yy}, {1,u,v} x {xe,ye}
+__device__ __forceinline__ void values_3cp(const int S[5], long long u, long long v, long long* o) {
+  const long long mono[6] = {1, u, v, u * u, u * v, v * v};
+#pragma unroll
+  for (int s = 0; s < 3; s++)
+#pragma unroll
+    for (int k = 0; k < 6; k++) o[s * 6 + k] += mono[k] * (long long)S[s];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    o[18 + k] += mono[k] * (long long)S[3];
+    o[21 + k] += mono[k] * (long long)S[4];
+  }
+}
+
+// 3-CP regressors as linear forms in (1, u, v): iC_c = alpha_c . gx + beta_c . gy
+// (gx, u gx, gy, u gy, v gx, v gy); product of two forms against the moments.
+__device__ __forceinline__ long long qf(const int* p, const int* q, const long long* m) {
+  return (long long)(p[0] * q[0]) * m[0] + (long long)(p[0] * q[1] + p[1] * q[0]) * m[1] +
+         (long long)(p[0] * q[2] + p[2] * q[0]) * m[2] + (long long)(p[1] * q[1]) * m[3] +
+         (long long)(p[1] * q[2] + p[2] * q[1]) * m[4] + (long long)(p[2] * q[2]) * m[5];
+}
+
+// VTM solveEqual (affine.cl:782-856) on R[r] = private_dEqualCoeff[r + 1]
+// (affine.cl:759-763), all indices static so the system stays in registers:
+// pivot search with the sequential strict-'>' scan (NaN never wins), row swap,
+// elimination a[j][k] -= a[i][k] * a[j][i-1] / a[i][i-1] (no zero-pivot guard),
+// back-substitution with fma (FP_CONTRACT) and the zero-pivot reset.
+template <int N>
+__device__ __forceinline__ void solve_equal(double (&R)[N][N + 1], double (&p)[N]) {
 #pragma unroll
   for (int i = 1; i < N; i++) {
-    double temp = fabs(__shfl(a[i - 1], base + i - 1));
-    int tempIdx = i;
+    double temp = fabs(R[i - 1][i - 1]);
+    int idx = i - 1;
 #pragma unroll
-    for (int r = i + 1; r <= N; r++) {
-      const double f = fabs(__shfl(a[i - 1], base + r - 1));
+    for (int r = i; r < N; r++) {
+      const double f = fabs(R[r][i - 1]);
       if (f > temp) {
         temp = f;
-        tempIdx = r;
+        idx = r;
       }
     }
-    const int src = myRow == i ? tempIdx : (myRow == tempIdx ? i : myRow);
 #pragma unroll
-    for (int c = 0; c <= N; c++) a[c] = __shfl(a[c], base + (src - 1));
-    double P[N + 1];
+    for (int r = i; r < N; r++) {
+      const bool sw = idx == r;
 #pragma unroll
-    for (int c = i - 1; c <= N; c++) P[c] = __shfl(a[c], base + i - 1);
-    if (myRow > i) {
-      const double f = a[i - 1];
+      for (int c = 0; c <= N; c++) {
+        const double a = R[i - 1][c], b = R[r][c];
+        R[i - 1][c] = sw ? b : a;
+        R[r][c] = sw ? a : b;
+      }
+    }
 #pragma unroll
-      for (int k = i; k <= N; k++) a[k] = __dsub_rn(a[k], __ddiv_rn(__dmul_rn(P[k], f), P[i - 1]));
+    for (int r = i; r < N; r++) {
+      const double f = R[r][i - 1];
+#pragma unroll
+      for (int k = i; k <= N; k++)
+        R[r][k] = __dsub_rn(R[r][k], __ddiv_rn(__dmul_rn(R[i - 1][k], f), R[i - 1][i - 1]));
     }
   }
 #pragma unroll
   for (int k = 0; k < N; k++) p[k] = 0.;
-  p[N - 1] = __shfl(__ddiv_rn(a[N], a[N - 1]), base + N - 1);
+  p[N - 1] = __ddiv_rn(R[N - 1][N], R[N - 1][N - 1]);
   bool zero = false;
 #pragma unroll
   for (int i = N - 2; i >= 0; i--) {
-    double temp = 0;
-#pragma unroll
-    for (int jj = i + 1; jj < N; jj++) temp = fma(a[jj], p[jj], temp);
-    const double val = __ddiv_rn(__dsub_rn(a[N], temp), a[i]);
-    const double pi = __shfl(val, base + i);
-    const int z = __shfl((int)(a[i] == 0.), base + i);
     if (!zero) {
-      if (z)
+      if (R[i][i] == 0.) {
         zero = true;
-      else
-        p[i] = pi;
+      } else {
+        double temp = 0;
+#pragma unroll
+        for (int j = i + 1; j < N; j++) temp = fma(R[i][j], p[j], temp);
+        p[i] = __ddiv_rn(__dsub_rn(R[i][N], temp), R[i][i]);
+      }
     }
   }
   if (zero) {
@@ -276,42 +570,123 @@ __device__ __forceinline__ void group_solve(const long long* __restrict__ M, boo
   }
 }
 
+// One CU's equations (reduced values V) -> the deltas fed to scaleDeltaMvs
+// (affine.cl:860-883).
+template <int NCP>
+__device__ __forceinline__ void solve_cu(const long long* V, int lw, int lh, double dd[6]) {
+  constexpr int N = 2 * NCP;
+  double R[N][N + 1];
+  if constexpr (NCP == 2) {
+    const long long A[4][4] = {{V[0], V[1], V[2], V[3]},
+                               {V[1], V[4], V[5], V[6]},
+                               {V[2], V[5], V[7], V[8]},
+                               {V[3], V[6], V[8], V[9]}};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) R[c][r] = (double)A[c][r];
+      R[c][4] = (double)(V[10 + c] * 8);  // rhs << 3 (affine.cl:705)
+    }
+  } else {
+    constexpr int al[6][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1}, {0, 0, 0}};
+    constexpr int be[6][3] = {{0, 0, 0}, {0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 0}, {0, 0, 1}};
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+#pragma unroll
+      for (int r = 0; r < 6; r++)
+        R[c][r] = (double)(qf(al[c], al[r], V + 0) + qf(al[c], be[r], V + 6) +
+                           qf(be[c], al[r], V + 6) + qf(be[c], be[r], V + 12));
+      long long b = 0;
+#pragma unroll
+      for (int k = 0; k < 3; k++) b += (long long)al[c][k] * V[18 + k] + (long long)be[c][k] * V[21 + k];
+      R[c][6] = (double)(b * 8);
+    }
+  }
+  double p[N];
+  solve_equal<N>(R, p);
+  const double w = (double)(1 << lw), h = (double)(1 << lh);
+  dd[0] = p[0];
+  dd[2] = p[2];
+  dd[1] = __dadd_rn(__dmul_rn(p[1], w), p[0]);  // exact scaling by a power of two
+  if constexpr (NCP == 3) {
+    dd[3] = __dadd_rn(__dmul_rn(p[3], w), p[2]);
+    dd[4] = __dadd_rn(__dmul_rn(p[4], h), p[0]);
+    dd[5] = __dadd_rn(__dmul_rn(p[5], h), p[2]);
+  } else {
+    dd[3] = __dadd_rn(__dmul_rn(-p[3], w), p[2]);
+    dd[4] = dd[5] = 0.;
+  }
+}
+
 struct CuState {  // 64 bytes
   int32_t cur[6];
   int32_t best[6];
   int64_t bestCost;
-  uint32_t satd;
+  int32_t satd;
   int32_t inframe;
   int32_t pad[2];
 };
 
 template <int REGION>
 struct Cfg {
-  static constexpr int SBPL = REGION == 128 ? 4 : 1;        // sub-blocks per lane
-  static constexpr int TILE = REGION + 2 * kMargin;         // tile edge (samples)
-  static constexpr int TP = REGION == 128 ? 176 : 112;      // tile pitch, == 16 (mod 32)
+  static constexpr int SBPL = REGION == 128 ? 4 : 1;    // sub-blocks per lane
+  static constexpr int TILE = REGION + 2 * kMargin;     // tile edge (samples)
+  static constexpr int TP = REGION == 128 ? 176 : 112;  // tile pitch (samples), == 16 (mod 32)
   static constexpr int TILE_ELEMS = TILE * TP + 16;
+  static constexpr int PRED_ELEMS = REGION * REGION + 2 * kPredPad + 8;
 };
 
-// VAME_ABLATE (timing-only builds, results are wrong): bit 0 skip the solve,
-// bit 1 skip gradient/moment math, bit 2 skip the moment reduction,
-// bit 3 skip the prediction math.
-#ifndef VAME_ABLATE
-#define VAME_ABLATE 0
-#endif
+// The reduced equations of this lane's sub-blocks for one CU: leader lanes of
+// each segment store (autonomous) or add (cooperative) into LDS.
+template <int NV, int SBPL, bool THREE>
+__device__ __forceinline__ void gradient_phase(bool active, int localSb0, int lcols, const Geo& g,
+                                               const uint16_t* __restrict__ cur, int W,
+                                               const uint16_t* s_pred, int segS, int segMax,
+                                               bool leader, bool coop, long long* dst) {
+  long long val[NV];
+#pragma unroll
+  for (int i = 0; i < NV; i++) val[i] = 0;
+  if (active && !(VAME_ABLATE & 2)) {
+#pragma unroll 1
+    for (int j = 0; j < SBPL; j++) {
+      const int local = localSb0 + j;
+      const int sx = (local & ((1 << lcols) - 1)) << 2, sy = (local >> lcols) << 2;
+      int S[5];
+      grad_sb(sx, sy, g, cur, W, s_pred, S);
+      if (THREE)
+        values_3cp(S, sx + 2, sy + 2, val);
+      else
+        values_2cp(S, sx + 2, sy + 2, val);
+    }
+  }
+  if (VAME_ABLATE & 4) return;
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    const long long v = seg_sum64(val[i], segS, segMax);
+    if (leader) {
+      if (coop)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&dst[i]), (unsigned long long)v);
+      else
+        dst[i] = v;
+    }
+  }
+}
 
 template <int REGION>
 __device__ __forceinline__ void affine_me_body(const KParams& p) {
   using C = Cfg<REGION>;
   __shared__ __attribute__((aligned(16))) uint16_t s_tile[C::TILE_ELEMS];
-  __shared__ __attribute__((aligned(16))) uint16_t s_pred[REGION * REGION];
-  __shared__ __attribute__((aligned(16))) long long s_mom[kMaxCu][kNumMom];
+  __shared__ __attribute__((aligned(16))) uint16_t s_predBuf[C::PRED_ELEMS];
+  __shared__ __attribute__((aligned(16))) long long s_val[kMaxCu][kNumMom];
+  __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
   __shared__ CuState s_st[kMaxCu];
   __shared__ CuSlot s_cu[kMaxCu];
+  __shared__ WaveDesc s_wave[kMaxWaves];
   __shared__ int s_hdr[4];
+  uint16_t* s_pred = s_predBuf + kPredPad;
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63;
+  const int lane = tid & 63, wv = tid >> 6;
 
   // ---- XCD-aware block -> (ref, ctu, item): blocks b, b+8, ... share an XCD;
   // give each XCD a contiguous run of logical work (same CTUs -> L2 reuse).
@@ -328,26 +703,26 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   const int W = p.W, H = p.H;
   const int ctuX = (ctu % p.ctusPerRow) * kCtu, ctuY = (ctu / p.ctusPerRow) * kCtu;
 
-  if (tid < kMaxCu) {
-    s_cu[tid] = it->cu[tid];
-  }
+  if (tid < kMaxCu) s_cu[tid] = it->cu[tid];
+  if (tid < kMaxWaves) s_wave[tid] = it->wave[tid];
+  if (tid < 48) s_coef[tid] = reinterpret_cast<const uint4*>(&kCoefTab)[tid];
   if (tid == 0) {
     s_hdr[0] = it->nCu;
-    s_hdr[1] = it->nSb;
+    s_hdr[1] = it->nWaves | (it->coop << 8);
     s_hdr[2] = it->rx;
     s_hdr[3] = it->ry;
   }
   __syncthreads();
-  const int nCu = s_hdr[0], nSb = s_hdr[1];
-  const int fx0 = ctuX + s_hdr[2], fy0 = ctuY + s_hdr[3];  // region origin (frame)
-  const int tx0 = fx0 - kMargin, ty0 = fy0 - kMargin;     // tile origin (frame)
+  const int nCu = s_hdr[0], nWaves = s_hdr[1] & 0xFF;
+  const bool coop = (s_hdr[1] >> 8) != 0;
+  const int tx0 = ctuX + s_hdr[2] - kMargin, ty0 = ctuY + s_hdr[3] - kMargin;  // tile origin
 
   // ---- stage the reference region (+margin) into LDS, clamp-to-edge padded
   {
     constexpr int CPR = C::TILE / 4;  // 8-byte chunks per row
     for (int ch = tid; ch < C::TILE * CPR; ch += kThreads) {
-      int ty = ch / CPR, cx = (ch % CPR) * 4;
-      int fy = clampi(ty0 + ty, 0, H - 1), fx = tx0 + cx;
+      const int ty = ch / CPR, cx = (ch % CPR) * 4;
+      const int fy = clampi(ty0 + ty, 0, H - 1), fx = tx0 + cx;
       const uint16_t* row = ref + (size_t)fy * W;
       uint2 v;
       if (fx >= 0 && fx + 3 < W) {
@@ -361,33 +736,53 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       *reinterpret_cast<uint2*>(&s_tile[ty * C::TP + cx]) = v;
     }
   }
+  if (tid < kMaxCu * kNumMom) (&s_val[0][0])[tid] = 0;
+  if (tid + kThreads < kMaxCu * kNumMom) (&s_val[0][0])[tid + kThreads] = 0;
+  if (tid + 2 * kThreads < kMaxCu * kNumMom) (&s_val[0][0])[tid + 2 * kThreads] = 0;
+  __syncthreads();
+  if (!coop && wv >= nWaves) return;  // wave-uniform: an autonomous wave without CUs
 
-  // ---- per-lane sub-block assignment (fixed for the whole item)
-  int myCu = -1;  // CU slot of this lane's sub-block(s)
-  {
-    const int t0 = tid * C::SBPL;
-    if (t0 < nSb) {
-      int k = 0;
-      for (int j = 1; j < nCu; j++)
-        if (s_cu[j].sbBase <= t0) k = j;
-      myCu = k;
-    }
+  // ---- this wave's per-CU lanes, this lane's CU and sub-blocks (fixed per item)
+  int cuB = 0, nCuW = 0, lidx = tid, nSbScope = 0, kEnd = nCu;
+  if (coop) {
+    nCuW = wv == 0 ? nCu : 0;
+    kEnd = nCu;
+    nSbScope = it->nSb;
+  } else {
+    const WaveDesc wd = s_wave[wv];
+    cuB = wd.cuBegin;
+    nCuW = wd.cuEnd - wd.cuBegin;
+    kEnd = wd.cuEnd;
+    nSbScope = wd.nSb;
+    lidx = lane;
   }
-  int cuW = 0, cuH = 0, cuLw = 0, cuLh = 0, cuX = 0, cuY = 0, predBase = 0, segS = 1;
+  int myCu = -1;
+  if (lidx * C::SBPL < nSbScope) {
+    int k = cuB;
+    for (int j = cuB + 1; j < kEnd; j++)
+      if (s_cu[j].laneBase <= lidx) k = j;
+    myCu = k;
+  }
+  Geo g;
+  g.x = g.y = g.lw = g.lh = g.w = g.h = g.predBase = 0;
+  int segS = 1, localSb0 = 0;
   bool active = false;
   if (myCu >= 0) {
     const CuSlot cs = s_cu[myCu];
-    cuLw = cs.lw;
-    cuLh = cs.lh;
-    cuW = 1 << cuLw;
-    cuH = 1 << cuLh;
-    cuX = ctuX + cs.x;
-    cuY = ctuY + cs.y;
-    predBase = cs.sbBase * 16;
-    segS = min(((cuW * cuH) >> 4) / C::SBPL, 64);
-    active = (cuX + cuW <= W) && (cuY + cuH <= H);  // affine.cl:192-193
+    g.lw = cs.lw;
+    g.lh = cs.lh;
+    g.w = 1 << g.lw;
+    g.h = 1 << g.lh;
+    g.x = ctuX + cs.x;
+    g.y = ctuY + cs.y;
+    g.predBase = cs.sbBase * 16;
+    segS = min(((g.w * g.h) >> 4) / C::SBPL, 64);
+    localSb0 = (lidx - cs.laneBase) * C::SBPL;
+    active = (g.x + g.w <= W) && (g.y + g.h <= H);  // affine.cl:192-193
   }
+  const bool leader = myCu >= 0 && (lane & (segS - 1)) == 0;
   const int segMax = wave_max_pow2(segS);
+  const int lcols = g.lw - 2;  // log2 of the CU's sub-block columns
 
   for (int pass = 0; pass < 2; pass++) {
     const int ncp = pass == 0 ? 2 : 3;
@@ -395,22 +790,23 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     const int niter = (ncp == 3 ? 4 : 5) + p.extra;
 
     // ---- per-CU initial CPMVs (2 CP: zero; 3 CP: derived from the 2-CP winner)
-    if (tid < nCu) {
-      const CuSlot cs = s_cu[tid];
-      CuState& st = s_st[tid];
+    if (lane < nCuW) {
+      const int k = cuB + lane;
+      const CuSlot cs = s_cu[k];
+      CuState& st = s_st[k];
       const int cx = ctuX + cs.x, cy = ctuY + cs.y;
       int c[6] = {0, 0, 0, 0, 0, 0};
       if (ncp == 3) {
-        int prev[6];
+        int prev[4];
         if (p.run2) {
-          for (int i = 0; i < 6; i++) prev[i] = st.best[i];
+          for (int i = 0; i < 4; i++) prev[i] = st.best[i];
         } else {
           const vame_cpmvs_dev& pv =
               p.prev[cs.align][(size_t)ctu * (cs.align ? kHalfCusPerCtu : kFullCusPerCtu) + cs.outOff];
           prev[0] = pv.ltx; prev[1] = pv.lty; prev[2] = pv.rtx; prev[3] = pv.rty;
         }
         // affine.cl:81-105
-        int sh = 7 + cs.lh - cs.lw;
+        const int sh = 7 + cs.lh - cs.lw;
         int vx2 = shl(prev[0], 7) - shl(prev[3] - prev[1], sh);
         int vy2 = shl(prev[1], 7) + shl(prev[2] - prev[0], sh);
         vx2 = (vx2 + 64 - (vx2 >= 0)) >> 7;
@@ -429,155 +825,52 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       st.bestCost = kCostInit;
       st.satd = 0;
       st.inframe = (cx + (1 << cs.lw) <= W) && (cy + (1 << cs.lh) <= H);
-      for (int i = 0; i < kNumMom; i++) s_mom[tid][i] = 0;
     }
-    __syncthreads();
+    phase_sync(coop);
 
     for (int iter = 0; iter <= niter; iter++) {
       // =============== prediction + SATD (affine.cl:208-393) ===============
       int satdLane = 0;
       if (active && !(VAME_ABLATE & 8)) {
-        const CuState& st = s_st[myCu];
         int cp[6];
-        for (int i = 0; i < 6; i++) cp[i] = st.cur[i];
-        // deriveMv{2,3}Cps_and_spread (aux_functions.cl:146-212)
-        const int hx = shl(cp[2] - cp[0], 7 - cuLw), hy = shl(cp[3] - cp[1], 7 - cuLw);
-        int vx, vy;
-        if (ncp == 3) {
-          vx = shl(cp[4] - cp[0], 7 - cuLh);
-          vy = shl(cp[5] - cp[1], 7 - cuLh);
-        } else {
-          vx = -hy;
-          vy = hx;
-        }
-        const bool spread = spread_over_limit(hx, hy, vx, vy);
-        const int bx = shl(cp[0], 7), by = shl(cp[1], 7);
+        for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
+        const MvField f = mv_field(cp, ncp, g.lw, g.lh);
+#pragma unroll 1
         for (int j = 0; j < C::SBPL; j++) {
-          int local = (tid * C::SBPL + j) - s_cu[myCu].sbBase;
-          int lcols = cuLw - 2;
-          int sx = (local & ((1 << lcols) - 1)) << 2, sy = (local >> lcols) << 2;
-          int px = spread ? (cuW >> 1) : sx + 2, py = spread ? (cuH >> 1) : sy + 2;
-          int mx = bx + hx * px + vx * py, my = by + hy * px + vy * py;
-          mx = (mx + 64 - (mx >= 0)) >> 7;
-          my = (my + 64 - (my >= 0)) >> 7;
-          clip_mv(mx, my, cuX, cuY, W, H);
-          const int ix = mx >> 4, fxr = mx & 15, iy = my >> 4, fyr = my & 15;
-          const int wx = cuX + sx + ix - 2, wy = cuY + sy + iy - 2;  // 9x9 window origin
-          const int tx = wx - tx0, ty = wy - ty0;
-          const bool inTile = (unsigned)tx <= (unsigned)(C::TILE - 9) &&
-                              (unsigned)ty <= (unsigned)(C::TILE - 9);
-          int cfx[6], cfy[6];
-          luma_coeffs(fxr, cfx);
-          luma_coeffs(fyr, cfy);
-          int tmp[9][4];
-#pragma unroll
-          for (int i = 0; i < 9; i++) {
-            int w9[9];
-            if (inTile) {
-              const int base = (ty + i) * C::TP + (tx & ~3);
-              const uint2* src = reinterpret_cast<const uint2*>(&s_tile[base]);
-              uint2 q0 = src[0], q1 = src[1], q2 = src[2];
-              unsigned d[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
-              const int s = tx & 3;
-              if (s & 2) {
-#pragma unroll
-                for (int k = 0; k < 5; k++) d[k] = d[k + 1];
-              }
-              if (s & 1) {
-#pragma unroll
-                for (int k = 0; k < 5; k++) d[k] = __builtin_amdgcn_alignbit(d[k + 1], d[k], 16);
-              }
-#pragma unroll
-              for (int m = 0; m < 9; m++) w9[m] = (d[m >> 1] >> ((m & 1) * 16)) & 0xFFFF;
-            } else {
-              const uint16_t* row = ref + (size_t)clampi(wy + i, 0, H - 1) * W;
-#pragma unroll
-              for (int m = 0; m < 9; m++) w9[m] = row[clampi(wx + m, 0, W - 1)];
-            }
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-              int sum = 0;
-#pragma unroll
-              for (int m = 0; m < 6; m++) sum += __mul24(w9[c + m], cfx[m]);
-              tmp[i][c] = (sum - 32768) >> 2;  // offset -IF_INTERNAL_OFFS<<2, shift 2
-            }
-          }
-          int pr[16];
-#pragma unroll
-          for (int r = 0; r < 4; r++)
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-              int sum = 0;
-#pragma unroll
-              for (int m = 0; m < 6; m++) sum += __mul24(tmp[r + m][c], cfy[m]);
-              pr[r * 4 + c] = clampi((sum + 512 + (8192 << 6)) >> 10, 0, 1023);
-            }
-          // store prediction (CU-compact layout) and SATD vs the original
-          int diff[16];
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const int ofs = predBase + (sy + r) * cuW + sx;
-            uint2 pk;
-            pk.x = (unsigned)pr[r * 4 + 0] | ((unsigned)pr[r * 4 + 1] << 16);
-            pk.y = (unsigned)pr[r * 4 + 2] | ((unsigned)pr[r * 4 + 3] << 16);
-            *reinterpret_cast<uint2*>(&s_pred[ofs]) = pk;
-            const uint2 o = *reinterpret_cast<const uint2*>(cur + (size_t)(cuY + sy + r) * W + cuX + sx);
-            diff[r * 4 + 0] = (int)(o.x & 0xFFFF) - pr[r * 4 + 0];
-            diff[r * 4 + 1] = (int)(o.x >> 16) - pr[r * 4 + 1];
-            diff[r * 4 + 2] = (int)(o.y & 0xFFFF) - pr[r * 4 + 2];
-            diff[r * 4 + 3] = (int)(o.y >> 16) - pr[r * 4 + 3];
-          }
-          // aux_functions.cl:1940-2043 (xCalcHADs4x4)
-          int m[16], d[16];
-          m[0] = diff[0] + diff[12]; m[1] = diff[1] + diff[13];
-          m[2] = diff[2] + diff[14]; m[3] = diff[3] + diff[15];
-          m[4] = diff[4] + diff[8];  m[5] = diff[5] + diff[9];
-          m[6] = diff[6] + diff[10]; m[7] = diff[7] + diff[11];
-          m[8] = diff[4] - diff[8];  m[9] = diff[5] - diff[9];
-          m[10] = diff[6] - diff[10]; m[11] = diff[7] - diff[11];
-          m[12] = diff[0] - diff[12]; m[13] = diff[1] - diff[13];
-          m[14] = diff[2] - diff[14]; m[15] = diff[3] - diff[15];
-          d[0] = m[0] + m[4];  d[1] = m[1] + m[5];  d[2] = m[2] + m[6];  d[3] = m[3] + m[7];
-          d[4] = m[8] + m[12]; d[5] = m[9] + m[13]; d[6] = m[10] + m[14]; d[7] = m[11] + m[15];
-          d[8] = m[0] - m[4];  d[9] = m[1] - m[5];  d[10] = m[2] - m[6]; d[11] = m[3] - m[7];
-          d[12] = m[12] - m[8]; d[13] = m[13] - m[9]; d[14] = m[14] - m[10]; d[15] = m[15] - m[11];
-          m[0] = d[0] + d[3];  m[1] = d[1] + d[2];  m[2] = d[1] - d[2];  m[3] = d[0] - d[3];
-          m[4] = d[4] + d[7];  m[5] = d[5] + d[6];  m[6] = d[5] - d[6];  m[7] = d[4] - d[7];
-          m[8] = d[8] + d[11]; m[9] = d[9] + d[10]; m[10] = d[9] - d[10]; m[11] = d[8] - d[11];
-          m[12] = d[12] + d[15]; m[13] = d[13] + d[14]; m[14] = d[13] - d[14]; m[15] = d[12] - d[15];
-          d[0] = m[0] + m[1];  d[1] = m[0] - m[1];  d[2] = m[2] + m[3];  d[3] = m[3] - m[2];
-          d[4] = m[4] + m[5];  d[5] = m[4] - m[5];  d[6] = m[6] + m[7];  d[7] = m[7] - m[6];
-          d[8] = m[8] + m[9];  d[9] = m[8] - m[9];  d[10] = m[10] + m[11]; d[11] = m[11] - m[10];
-          d[12] = m[12] + m[13]; d[13] = m[12] - m[13]; d[14] = m[14] + m[15]; d[15] = m[15] - m[14];
-          int sa = 0;
-#pragma unroll
-          for (int k = 1; k < 16; k++) sa += abs(d[k]);
-          sa += abs(d[0]) >> 2;
-          satdLane += (sa + 1) >> 1;
+          const int local = localSb0 + j;
+          const int sx = (local & ((1 << lcols) - 1)) << 2, sy = (local >> lcols) << 2;
+          satdLane += predict_sb<C::TILE, C::TP>(f, sx, sy, g, s_tile, tx0, ty0, ref, cur, W, H,
+                                                 s_pred, s_coef);
         }
       }
       {
-        int v = seg_sum32(satdLane, segS, segMax);
-        if (active && (lane & (segS - 1)) == 0) atomicAdd(&s_st[myCu].satd, (unsigned)v);
+        const int v = seg_sum32(satdLane, segS, segMax);
+        if (leader) {
+          if (coop)
+            atomicAdd(&s_st[myCu].satd, v);
+          else
+            s_st[myCu].satd = v;
+        }
       }
-      __syncthreads();
+      phase_sync(coop);
 
       // =============== cost, best update (affine.cl:416-457) ===============
       const bool lastIter = iter == niter;
-      if (tid < nCu) {
-        CuState& st = s_st[tid];
+      if (lane < nCuW) {
+        const int k = cuB + lane;
+        CuState& st = s_st[k];
         if (iter == 0 || st.inframe) {
           const int bits = affine_bits(st.cur, ncp) + kRuiBits;
           const float prod = __fmul_rn(p.lambda, (float)bits);
           const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
-          st.satd = 0;
           if (cost < st.bestCost) {
             st.bestCost = cost;
             for (int i = 0; i < 6; i++) st.best[i] = st.cur[i];
           }
         }
+        st.satd = 0;
         if (lastIter) {  // affine.cl:928-957
-          const CuSlot cs = s_cu[tid];
+          const CuSlot cs = s_cu[k];
           const int mode = cs.align * 2 + (ncp - 2);
           const size_t idx = (size_t)ctu * (cs.align ? kHalfCusPerCtu : kFullCusPerCtu) + cs.outOff;
           p.cost[refIdx][mode][idx] = st.bestCost;
@@ -590,141 +883,30 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       }
       if (lastIter) break;  // uniform
 
-      // =============== gradients + normal-equation moments (affine.cl:477-708) ===============
-      // per sub-block: S = (sum gx^2, gx gy, gy^2, gx e, gy e) over its 16 samples (int32 exact)
-      int S5[C::SBPL][5];
-      int su[C::SBPL], sv[C::SBPL];
-#pragma unroll
-      for (int j = 0; j < C::SBPL; j++) {
-        su[j] = sv[j] = 0;
-#pragma unroll
-        for (int k = 0; k < 5; k++) S5[j][k] = 0;
-      }
-      if (active && !(VAME_ABLATE & 2)) {
-#pragma unroll
-        for (int j = 0; j < C::SBPL; j++) {
-          int local = (tid * C::SBPL + j) - s_cu[myCu].sbBase;
-          int lcols = cuLw - 2;
-          int sx = (local & ((1 << lcols) - 1)) << 2, sy = (local >> lcols) << 2;
-          // 6x6 prediction patch around the sub-block, rows clamped into the CU;
-          // columns outside the CU only feed gradients that are replaced below.
-          int P[6][6];
-#pragma unroll
-          for (int i = 0; i < 6; i++) {
-            const int rr = clampi(sy - 1 + i, 0, cuH - 1);
-            const uint16_t* prow = &s_pred[predBase + rr * cuW];
-            const uint2 mid = *reinterpret_cast<const uint2*>(prow + sx);
-            const uint2 lft = *reinterpret_cast<const uint2*>(prow + max(sx - 4, 0));
-            const uint2 rgt = *reinterpret_cast<const uint2*>(prow + min(sx + 4, cuW - 4));
-            P[i][0] = (int)(lft.y >> 16);
-            P[i][1] = (int)(mid.x & 0xFFFF);
-            P[i][2] = (int)(mid.x >> 16);
-            P[i][3] = (int)(mid.y & 0xFFFF);
-            P[i][4] = (int)(mid.y >> 16);
-            P[i][5] = (int)(rgt.x & 0xFFFF);
-          }
-          int gx[4][4], gy[4][4];
-#pragma unroll
-          for (int r = 0; r < 4; r++)
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-              gx[r][c] = (P[r][c + 2] - P[r][c]) + 2 * (P[r + 1][c + 2] - P[r + 1][c]) +
-                         (P[r + 2][c + 2] - P[r + 2][c]);
-              gy[r][c] = (P[r + 2][c] - P[r][c]) + 2 * (P[r + 2][c + 1] - P[r][c + 1]) +
-                         (P[r + 2][c + 2] - P[r][c + 2]);
-            }
-          // CU-border replication (affine.cl:506-540): rows first, then columns
-          if (sy == 0) {
-#pragma unroll
-            for (int c = 0; c < 4; c++) { gx[0][c] = gx[1][c]; gy[0][c] = gy[1][c]; }
-          }
-          if (sy + 4 == cuH) {
-#pragma unroll
-            for (int c = 0; c < 4; c++) { gx[3][c] = gx[2][c]; gy[3][c] = gy[2][c]; }
-          }
-          if (sx == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) { gx[r][0] = gx[r][1]; gy[r][0] = gy[r][1]; }
-          }
-          if (sx + 4 == cuW) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) { gx[r][3] = gx[r][2]; gy[r][3] = gy[r][2]; }
-          }
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const uint2 o = *reinterpret_cast<const uint2*>(cur + (size_t)(cuY + sy + r) * W + cuX + sx);
-            const int ov[4] = {(int)(o.x & 0xFFFF), (int)(o.x >> 16), (int)(o.y & 0xFFFF), (int)(o.y >> 16)};
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-              const int e = ov[c] - P[r + 1][c + 1];  // residual orig - pred (affine.cl:547-579)
-              const int a = gx[r][c], g = gy[r][c];
-              S5[j][0] += a * a;
-              S5[j][1] += a * g;
-              S5[j][2] += g * g;
-              S5[j][3] += a * e;
-              S5[j][4] += g * e;
-            }
-          }
-          su[j] = sx + 2;  // sub-block centre (affine.cl:680-681)
-          sv[j] = sy + 2;
-        }
-      }
-      // 24 exact moments per CU: sum over sub-blocks of {1,u,v,uu,uv,vv} x {Sxx,Sxy,Syy}
-      // and {1,u,v} x {Sxe,Sye}; wave segment reduction, then one LDS atomic per segment
-#pragma unroll
-      for (int i = 0; i < kNumMom; i++) {
-        if (VAME_ABLATE & 4) break;
-        long long v = 0;
-#pragma unroll
-        for (int j = 0; j < C::SBPL; j++) {
-          const int sidx = i < 18 ? i / 6 : (i < 21 ? 3 : 4);
-          const int mono = i < 18 ? i % 6 : (i - 18) % 3;
-          const long long u = su[j], w = sv[j];
-          const long long m = mono == 0 ? 1 : mono == 1 ? u : mono == 2 ? w : mono == 3 ? u * u
-                              : mono == 4 ? u * w : w * w;
-          v += m * (long long)S5[j][sidx];
-        }
-        v = seg_sum64(v, segS, segMax);
-        if (active && (lane & (segS - 1)) == 0)
-          atomicAdd(reinterpret_cast<unsigned long long*>(&s_mom[myCu][i]), (unsigned long long)v);
-      }
-      __syncthreads();
+      // =============== gradients + normal equations (affine.cl:477-752) ===============
+      long long* dst = s_val[myCu < 0 ? 0 : myCu];
+      if (ncp == 2)
+        gradient_phase<kNumVal2, C::SBPL, false>(active, localSb0, lcols, g, cur, W, s_pred, segS,
+                                                 segMax, leader, coop, dst);
+      else
+        gradient_phase<kNumMom, C::SBPL, true>(active, localSb0, lcols, g, cur, W, s_pred, segS,
+                                               segMax, leader, coop, dst);
+      phase_sync(coop);
 
-      // =============== solve + CPMV update (affine.cl:726-893), 8 lanes per CU ===============
-      {
-        const int g = tid >> 3;  // CU slot of this lane group
-        const bool act = g < nCu && s_st[g].inframe && !(VAME_ABLATE & 1);
-        const long long* M = s_mom[g < kMaxCu ? g : 0];
-        double pr[6] = {0, 0, 0, 0, 0, 0};
-        if (!__any(act)) {
-          // no live CU in this wave: nothing to solve
-        } else if (ncp == 3) {
-          double q[6];
-          group_solve<3>(M, act, lane, q);
+      // =============== solve + CPMV update (affine.cl:782-893), one lane per CU ===============
+      if (lane < nCuW && !(VAME_ABLATE & 1)) {
+        const int k = cuB + lane;
+        CuState& st = s_st[k];
+        if (st.inframe) {
+          const CuSlot cs = s_cu[k];
+          double dd[6];
+          if (ncp == 3)
+            solve_cu<3>(s_val[k], cs.lw, cs.lh, dd);
+          else
+            solve_cu<2>(s_val[k], cs.lw, cs.lh, dd);
+          if (coop) {
 #pragma unroll
-          for (int k = 0; k < 6; k++) pr[k] = q[k];
-        } else {
-          double q[4];
-          group_solve<2>(M, act, lane, q);
-#pragma unroll
-          for (int k = 0; k < 4; k++) pr[k] = q[k];
-        }
-        if (act && (tid & 7) == 0) {
-          CuState& st = s_st[g];
-          const CuSlot cs = s_cu[g];
-#pragma unroll
-          for (int i = 0; i < kNumMom; i++) s_mom[g][i] = 0;
-          double dd[6] = {0, 0, 0, 0, 0, 0};
-          const double w = (double)(1 << cs.lw), h = (double)(1 << cs.lh);
-          dd[0] = pr[0];
-          dd[2] = pr[2];
-          dd[1] = __dadd_rn(__dmul_rn(pr[1], w), pr[0]);  // exact scaling by a power of two
-          if (ncp == 3) {
-            dd[3] = __dadd_rn(__dmul_rn(pr[3], w), pr[2]);
-            dd[4] = __dadd_rn(__dmul_rn(pr[4], h), pr[0]);
-            dd[5] = __dadd_rn(__dmul_rn(pr[5], h), pr[2]);
-          } else {
-            dd[3] = __dadd_rn(__dmul_rn(-pr[3], w), pr[2]);
+            for (int i = 0; i < kNumMom; i++) s_val[k][i] = 0;
           }
           // affine.cl:884-893 (scaleDeltaMvs order: LT=(d0,d2), RT=(d1,d3), LB=(d4,d5))
           int c6[6];
@@ -744,9 +926,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           for (int i = 0; i < 6; i++) st.cur[i] = c6[i];
         }
       }
-      __syncthreads();
+      phase_sync(coop);
     }
-    __syncthreads();
+    phase_sync(coop);
   }
 }
 
