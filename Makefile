@@ -21,10 +21,11 @@ all: lib oracle
 
 lib: $(LIBDIR)/libvame.so
 
-# timing-only ablation builds (results are wrong): make ablate
+# timing-only ablation builds (results are wrong): make ablate [ABLATE_SET="..."]
+ABLATE_SET ?= 1 2 4 6 7 8 11 13 14 15 16 32
 ablate:
 	@mkdir -p $(LIBDIR)
-	for a in 1 2 4 6 7 8 11 13 14 15; do $(HIPCC) $(HIPFLAGS) -DVAME_ABLATE=$$a -shared -o $(LIBDIR)/libvame_ablate$$a.so $(LIB_SRCS) || exit 1; done
+	for a in $(ABLATE_SET); do $(HIPCC) $(HIPFLAGS) -DVAME_ABLATE=$$a -shared -o $(LIBDIR)/libvame_ablate$$a.so $(LIB_SRCS) || exit 1; done
 cli: $(BINDIR)/vame
 
 $(LIBDIR)/libvame.so: $(LIB_SRCS) $(LIB_HDRS)

@@ -58,55 +58,12 @@ struct CuDesc {
   int x, y, w, h, align, outOff;
 };
 
-// One work item.  sbpl = sub-blocks per lane of the kernel class (1 quadrant,
-// 4 CTU).  Quadrant items whose CUs all fit one wave (<= 64 sub-blocks) are
-// "autonomous": CUs are first-fit packed into <= 4 waves of 64 lanes and every
-// wave refines its own CUs; other items are "cooperative" (CUs span waves,
-// workgroup barriers per phase).  In both modes larger CUs come first inside
-// their lane range, so every CU's first lane is aligned to its own
-// power-of-two lane count, which the segmented wave reductions rely on.
-Item make_item(int rx, int ry, std::vector<CuDesc> cus, int sbpl) {
-  std::stable_sort(cus.begin(), cus.end(),
-                   [](const CuDesc& a, const CuDesc& b) { return a.w * a.h > b.w * b.h; });
+int nsb_of(const CuDesc& c) { return c.w * c.h / 16; }
+
+void fill_slots(Item& it, const std::vector<CuDesc>& cus) {
   if ((int)cus.size() > kMaxCu) abort();
-  Item it;
-  memset(&it, 0, sizeof(it));
   it.nCu = (int16_t)cus.size();
-  it.rx = (int16_t)rx;
-  it.ry = (int16_t)ry;
-  bool coop = sbpl > 1;
-  for (auto& c : cus) coop |= c.w * c.h / 16 > 64;
-  std::vector<int> waveOf(cus.size(), 0);
-  int nWaves = 1;
-  if (!coop) {
-    int fill[kMaxWaves] = {0, 0, 0, 0};
-    nWaves = 0;
-    for (size_t k = 0; k < cus.size(); k++) {
-      const int nsb = cus[k].w * cus[k].h / 16;
-      int w = 0;
-      while (w < nWaves && fill[w] + nsb > 64) w++;
-      if (w == nWaves) nWaves++;
-      if (nWaves > kMaxWaves) abort();
-      fill[w] += nsb;
-      waveOf[k] = w;
-    }
-    // CU slots grouped by wave (stable: still largest first inside a wave)
-    std::vector<size_t> order(cus.size());
-    for (size_t k = 0; k < order.size(); k++) order[k] = k;
-    std::stable_sort(order.begin(), order.end(),
-                     [&](size_t a, size_t b) { return waveOf[a] < waveOf[b]; });
-    std::vector<CuDesc> c2;
-    std::vector<int> w2;
-    for (size_t k : order) {
-      c2.push_back(cus[k]);
-      w2.push_back(waveOf[k]);
-    }
-    cus.swap(c2);
-    waveOf.swap(w2);
-  }
-  it.coop = coop ? 1 : 0;
-  it.nWaves = (int16_t)(coop ? kMaxWaves : nWaves);
-  int sb = 0, waveSb0 = 0, prevWave = -1;
+  int sb = 0;
   for (size_t k = 0; k < cus.size(); k++) {
     CuSlot& s = it.cu[k];
     s.x = (int16_t)cus[k].x;
@@ -116,30 +73,81 @@ Item make_item(int rx, int ry, std::vector<CuDesc> cus, int sbpl) {
     s.align = (uint8_t)cus[k].align;
     s.outOff = (int16_t)cus[k].outOff;
     s.sbBase = (int16_t)sb;
-    if (coop) {
-      s.laneBase = (int16_t)(sb / sbpl);
-    } else {
-      const int w = waveOf[k];
-      if (w != prevWave) {
-        it.wave[w].cuBegin = (int16_t)k;
-        waveSb0 = sb;
-        prevWave = w;
-      }
-      it.wave[w].cuEnd = (int16_t)(k + 1);
-      it.wave[w].nSb = (int16_t)(sb + cus[k].w * cus[k].h / 16 - waveSb0);
-      s.laneBase = (int16_t)(sb - waveSb0);
-    }
-    sb += cus[k].w * cus[k].h / 16;
+    sb += nsb_of(cus[k]);
   }
-  it.nSb = (int16_t)sb;
-  if (sb > kThreads * sbpl) abort();
+}
+
+// Cooperative item: CUs of one size, each spanning nsb >= 64 lanes (one per
+// sub-block) of the workgroup (workgroup barriers per phase, LDS atomics).
+Item make_coop_item(int rx, int ry, const std::vector<CuDesc>& cus, int threads) {
+  Item it;
+  memset(&it, 0, sizeof(it));
+  it.rx = (int16_t)rx;
+  it.ry = (int16_t)ry;
+  it.coop = 1;
+  it.nWaves = kMaxWaves;
+  const int nsb = nsb_of(cus[0]);
+  for (auto& c : cus)
+    if (nsb_of(c) != nsb) abort();
+  if (nsb < 64 || (int)cus.size() * nsb > threads) abort();
+  it.logL = (int16_t)ilog2(nsb);
+  fill_slots(it, cus);
   return it;
 }
 
+// Autonomous item: up to 4 waves, each holding CUs of ONE size (<= 64
+// sub-blocks, one lane per sub-block), so a wave's segment size is uniform.
+Item make_auto_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& waves) {
+  Item it;
+  memset(&it, 0, sizeof(it));
+  it.rx = (int16_t)rx;
+  it.ry = (int16_t)ry;
+  it.coop = 0;
+  if (waves.empty() || (int)waves.size() > kMaxWaves) abort();
+  it.nWaves = (int16_t)waves.size();
+  std::vector<CuDesc> all;
+  for (size_t w = 0; w < waves.size(); w++) {
+    const int nsb = nsb_of(waves[w][0]);
+    int used = 0;
+    for (auto& c : waves[w]) {
+      if (nsb_of(c) != nsb) abort();
+      used += nsb;
+    }
+    if (used > 64) abort();
+    it.wave[w].cuBegin = (int16_t)all.size();
+    all.insert(all.end(), waves[w].begin(), waves[w].end());
+    it.wave[w].cuEnd = (int16_t)all.size();
+    it.wave[w].logL = (int16_t)ilog2(nsb);
+  }
+  fill_slots(it, all);
+  return it;
+}
+
+// CUs of one quadrant and one alignment, <= 64 sub-blocks: waves of one size
+// class (largest first), then items of 4 consecutive waves.
+void pack_autonomous(int qx, int qy, std::vector<CuDesc> cus, std::vector<Item>& out) {
+  std::stable_sort(cus.begin(), cus.end(),
+                   [](const CuDesc& a, const CuDesc& b) { return nsb_of(a) > nsb_of(b); });
+  std::vector<std::vector<CuDesc>> waves;
+  for (auto& c : cus) {
+    if (waves.empty() || nsb_of(waves.back()[0]) != nsb_of(c) ||
+        (int)(waves.back().size() + 1) * nsb_of(c) > 64)
+      waves.push_back({});
+    waves.back().push_back(c);
+  }
+  for (size_t w = 0; w < waves.size(); w += kMaxWaves) {
+    std::vector<std::vector<CuDesc>> grp(waves.begin() + w,
+                                         waves.begin() + std::min(waves.size(), w + kMaxWaves));
+    out.push_back(make_auto_item(qx, qy, grp));
+  }
+}
+
 // Work-item templates (identical for every CTU):
-//   big      : FULL 128x128 / 128x64 / 64x128 groups, whole CTU, 1024 sub-blocks
-//   quadFull : FULL groups <= 64x64, one item per (group, 64x64 quadrant), 256 sub-blocks
-//   quadHalf : HALF groups, per quadrant, first-fit-decreasing packed to <= 256 sub-blocks
+//   big      : FULL 128x128 / 128x64 / 64x128 groups, whole CTU, cooperative
+//   quadFull : FULL groups <= 64x64 per 64x64 quadrant: 64x64 / 64x32 / 32x64
+//              cooperative (one item per group), the rest autonomous
+//   quadHalf : HALF groups per quadrant (no HALF CU crosses a quadrant):
+//              64x32 + 32x64 cooperative, the rest autonomous
 void build_templates(std::vector<Item>& big, std::vector<Item>& quadFull,
                      std::vector<Item>& quadHalf) {
   for (int g = 0; g < kFullGroups; g++) {
@@ -147,51 +155,39 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& quadFull,
     if (w == 128 || h == 128) {
       std::vector<CuDesc> c;
       for (int k = 0; k < n; k++) c.push_back({(k % cols) * w, (k / cols) * h, w, h, 0, kFullStride[g] + k});
-      big.push_back(make_item(0, 0, c, Cfg<128>::SBPL));
-      continue;
-    }
-    for (int q = 0; q < 4; q++) {
-      const int qx = (q & 1) * 64, qy = (q >> 1) * 64;
-      std::vector<CuDesc> c;
-      for (int k = 0; k < n; k++) {
-        const int x = (k % cols) * w, y = (k / cols) * h;
-        if (x >= qx && x < qx + 64 && y >= qy && y < qy + 64) c.push_back({x, y, w, h, 0, kFullStride[g] + k});
-      }
-      quadFull.push_back(make_item(qx, qy, c, Cfg<64>::SBPL));
+      big.push_back(make_coop_item(0, 0, c, Cfg<128>::THREADS));
     }
   }
   for (int q = 0; q < 4; q++) {
     const int qx = (q & 1) * 64, qy = (q >> 1) * 64;
-    struct Grp { int sbTotal, sbPerCu; std::vector<CuDesc> cus; };
-    std::vector<Grp> groups;
-    for (int g = 0; g < kHalfGroups; g++) {
-      Grp gr;
-      gr.sbPerCu = kHalfW[g] * kHalfH[g] / 16;
-      gr.sbTotal = 0;
+    auto inq = [&](int x, int y) { return x >= qx && x < qx + 64 && y >= qy && y < qy + 64; };
+    std::vector<CuDesc> small;
+    for (int g = 0; g < kFullGroups; g++) {
+      const int w = kFullW[g], h = kFullH[g], n = (kCtu * kCtu) / (w * h), cols = kCtu / w;
+      if (w == 128 || h == 128) continue;
+      std::vector<CuDesc> c;
+      for (int k = 0; k < n; k++) {
+        const int x = (k % cols) * w, y = (k / cols) * h;
+        if (inq(x, y)) c.push_back({x, y, w, h, 0, kFullStride[g] + k});
+      }
+      if (w * h / 16 > 64)
+        quadFull.push_back(make_coop_item(qx, qy, c, Cfg<64>::THREADS));
+      else
+        small.insert(small.end(), c.begin(), c.end());
+    }
+    pack_autonomous(qx, qy, small, quadFull);
+    std::vector<CuDesc> bigHalf;
+    small.clear();
+    for (int g = 0; g < kHalfGroups; g++)
       for (int k = 0; k < kHalfN[g]; k++) {
         const int x = kHalfX8[g][k] * 8, y = kHalfY8[g][k] * 8;
-        if (x >= qx && x < qx + 64 && y >= qy && y < qy + 64) {
-          gr.cus.push_back({x, y, kHalfW[g], kHalfH[g], 1, kHalfStride[g] + k});
-          gr.sbTotal += gr.sbPerCu;
-        }
+        if (!inq(x, y)) continue;
+        if (x + kHalfW[g] > qx + 64 || y + kHalfH[g] > qy + 64) abort();
+        const CuDesc c{x, y, kHalfW[g], kHalfH[g], 1, kHalfStride[g] + k};
+        (nsb_of(c) > 64 ? bigHalf : small).push_back(c);
       }
-      if (!gr.cus.empty()) groups.push_back(gr);
-    }
-    std::stable_sort(groups.begin(), groups.end(),
-                     [](const Grp& a, const Grp& b) { return a.sbTotal > b.sbTotal; });
-    std::vector<std::pair<int, std::vector<CuDesc>>> bins;
-    for (auto& gr : groups) {
-      bool placed = false;
-      for (auto& bn : bins)
-        if (bn.first + gr.sbTotal <= kThreads && (int)(bn.second.size() + gr.cus.size()) <= kMaxCu) {
-          bn.first += gr.sbTotal;
-          bn.second.insert(bn.second.end(), gr.cus.begin(), gr.cus.end());
-          placed = true;
-          break;
-        }
-      if (!placed) bins.push_back({gr.sbTotal, gr.cus});
-    }
-    for (auto& bn : bins) quadHalf.push_back(make_item(qx, qy, bn.second, Cfg<64>::SBPL));
+    if (!bigHalf.empty()) quadHalf.push_back(make_coop_item(qx, qy, bigHalf, Cfg<64>::THREADS));
+    pack_autonomous(qx, qy, small, quadHalf);
   }
 }
 
@@ -234,6 +230,8 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
            hipStream_t stream) {
   // 128-class items (big LDS, 1 workgroup per CU) go first on a side stream so
   // they overlap with the quadrant items instead of forming a tail.
+  if (VAME_ABLATE & 16) bigItems = false;  // timing-only builds
+  if (VAME_ABLATE & 32) quadFull = quadHalf = false;
   const bool fork = bigItems && (quadFull || quadHalf);
   if (bigItems) {
     KParams kb = kp;
@@ -247,7 +245,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
       s = c->side;
     }
     VAME_TRY(time_begin(c, 1, s));
-    hipLaunchKernelGGL(affine_me_ctu, dim3(grid), dim3(kThreads), 0, s, kb);
+    hipLaunchKernelGGL(affine_me_ctu, dim3(grid), dim3(Cfg<128>::THREADS), 0, s, kb);
     VAME_HIP(hipGetLastError());
     VAME_TRY(time_end(c, 1, s));
     if (fork) VAME_HIP(hipEventRecord(c->evJoin, s));
@@ -258,7 +256,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
     const unsigned grid = (unsigned)(kq.nItems * kq.nCtus * kq.nRefs);
     VAME_TRY(time_begin(c, 0, stream));
-    hipLaunchKernelGGL(affine_me_quad, dim3(grid), dim3(kThreads), 0, stream, kq);
+    hipLaunchKernelGGL(affine_me_quad, dim3(grid), dim3(Cfg<64>::THREADS), 0, stream, kq);
     VAME_HIP(hipGetLastError());
     VAME_TRY(time_end(c, 0, stream));
   }

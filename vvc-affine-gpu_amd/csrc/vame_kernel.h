@@ -1,8 +1,8 @@
 // vame_kernel.h -- HIP/CDNA4 device code of the affine-ME hot path.
 //
-// One workgroup (256 threads = 4 waves) = one work item: a 64x64 quadrant of a
-// CTU (kernel affine_me_quad) or, for the 128-wide/high aligned sizes, the
-// whole 128x128 CTU (kernel affine_me_ctu), for one reference frame, holding
+// One workgroup = one work item: a 64x64 quadrant of a CTU (kernel
+// affine_me_quad, 256 threads) or, for the 128-wide/high aligned sizes, the
+// whole 128x128 CTU (kernel affine_me_ctu, 1024 threads), for one reference frame, holding
 // the candidate CUs of one or more CU-size groups.  The workgroup runs the
 // complete gradient-based CPMV refinement of affine.cl:195-917 for all of them
 // -- 2 control points, then 3 control points seeded from the 2-CP winner of
@@ -38,13 +38,12 @@
 
 namespace vame {
 
-constexpr int kMaxCu = 32;    // CU slots per work item
+constexpr int kMaxCu = 16;    // CU slots per work item
 constexpr int kMaxWaves = 4;
 constexpr int kMargin = 16;   // LDS reference-tile margin around the work-item region
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;  // quadrant workgroups
 constexpr int kNumMom = 24;   // 3 CP: {1,u,v,uu,uv,vv} x {xx,xy,yy} + {1,u,v} x {xe,ye}
 constexpr int kNumVal2 = 14;  // 2 CP: 10 distinct matrix entries + 4 right-hand sides
-constexpr int kPredPad = 8;   // samples in front of the LDS prediction buffer
 
 // device view of vame_cpmvs / typedef.h Cpmvs (28 bytes)
 struct vame_cpmvs_dev {
@@ -58,19 +57,21 @@ struct CuSlot {     // 16 bytes
   uint8_t pad0;
   int16_t outOff;   // RETURN_STRIDE[group] + cuIdx
   int16_t sbBase;   // first sub-block of this CU inside the item (prediction buffer / 16)
-  int16_t laneBase; // first lane of this CU (wave lane when autonomous, thread when cooperative)
-  int16_t pad1;
+  int32_t pad1;
 };
 
-struct WaveDesc {   // 8 bytes: the CU slots a wave owns (autonomous items)
-  int16_t cuBegin, cuEnd, nSb, pad;
+struct WaveDesc {   // autonomous items: the CU slots a wave owns, all of one size
+  int16_t cuBegin, cuEnd;
+  int16_t logL;     // log2 lanes per CU (= sub-blocks per CU)
+  int16_t pad;
 };
 
 struct Item {
-  int16_t nCu, nSb;   // CU slots, sub-blocks
-  int16_t rx, ry;     // region origin (CTU-relative)
-  int16_t nWaves;     // waves holding CUs
-  int16_t coop;       // 1: cooperative mode
+  int16_t nCu;      // CU slots
+  int16_t rx, ry;   // region origin (CTU-relative)
+  int16_t coop;     // 1: cooperative (CUs span waves, all CUs of one size)
+  int16_t nWaves;   // autonomous: waves holding CUs
+  int16_t logL;     // cooperative: log2 lanes per CU (>= 6)
   int16_t pad0, pad1;
   WaveDesc wave[kMaxWaves];
   CuSlot cu[kMaxCu];
@@ -92,7 +93,8 @@ struct KParams {
 
 // VAME_ABLATE (timing-only builds, results are wrong): bit 0 skip the solve,
 // bit 1 skip the gradient math, bit 2 skip the reductions of the equations,
-// bit 3 skip the prediction math.
+// bit 3 skip the prediction math, bit 4 skip the 128-class launch, bit 5 skip
+// the quadrant launch.
 #ifndef VAME_ABLATE
 #define VAME_ABLATE 0
 #endif
@@ -178,49 +180,51 @@ __device__ __forceinline__ int scale_delta(double d) {
   return shl(cvt_i32_f64(d * 4.0 + s * 0.5), 2);
 }
 
-// Segment reduction over aligned power-of-two lane groups of size S (<= 64):
-// the FIRST lane of every segment ends with the segment total (other lanes hold
-// partial sums).  Steps inside a 16-lane DPP row use row_shl (bound_ctrl zero
-// fill), the cross-row steps use one shuffle each; `smax` (wave-uniform) bounds
-// the steps.  Must be called by every lane of the wave.
-template <int CTRL>
-__device__ __forceinline__ long long dpp_shl64(long long v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, 0xF, 0xF, true);
+// Segment sums over aligned segments of S lanes (S a power of two <= 64 and
+// UNIFORM across the wave -- the host packs every wave with CUs of one size):
+// the LAST lane of every segment ends with the segment total.  row_shr steps
+// inside a 16-lane DPP row (bound_ctrl: out-of-row sources read 0), then
+// row_bcast:15 / row_bcast:31 across rows (GFX9 DPP).  A segment's last lane
+// only ever adds lanes of its own segment, so no masking is needed.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWMASK, 0xF, true);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ long long dpp64(long long v) {
+  const int lo = dpp32<CTRL, ROWMASK>((int)v);
+  const int hi = dpp32<CTRL, ROWMASK>((int)(v >> 32));
   return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
-template <int CTRL>
-__device__ __forceinline__ int dpp_shl32(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+template <typename T>
+__device__ __forceinline__ T dpp_any(T v, int step) {
+  if constexpr (sizeof(T) == 8) {
+    switch (step) {
+      case 0: return dpp64<0x111, 0xF>(v);
+      case 1: return dpp64<0x112, 0xF>(v);
+      case 2: return dpp64<0x114, 0xF>(v);
+      case 3: return dpp64<0x118, 0xF>(v);
+      case 4: return dpp64<0x142, 0xA>(v);
+      default: return dpp64<0x143, 0xC>(v);
+    }
+  } else {
+    switch (step) {
+      case 0: return dpp32<0x111, 0xF>(v);
+      case 1: return dpp32<0x112, 0xF>(v);
+      case 2: return dpp32<0x114, 0xF>(v);
+      case 3: return dpp32<0x118, 0xF>(v);
+      case 4: return dpp32<0x142, 0xA>(v);
+      default: return dpp32<0x143, 0xC>(v);
+    }
+  }
 }
-__device__ __forceinline__ long long seg_sum64(long long v, int S, int smax) {
-  if (smax > 1) { long long o = dpp_shl64<0x101>(v); if (S > 1) v += o; }
-  if (smax > 2) { long long o = dpp_shl64<0x102>(v); if (S > 2) v += o; }
-  if (smax > 4) { long long o = dpp_shl64<0x104>(v); if (S > 4) v += o; }
-  if (smax > 8) { long long o = dpp_shl64<0x108>(v); if (S > 8) v += o; }
-  if (smax > 16) { long long o = __shfl_down(v, 16); if (S > 16) v += o; }
-  if (smax > 32) { long long o = __shfl_down(v, 32); if (S > 32) v += o; }
+// logS: log2 of the (wave-uniform, scalar) segment size
+template <typename T>
+__device__ __forceinline__ T seg_sum(T v, int logS) {
+#pragma unroll
+  for (int s = 0; s < 6; s++)
+    if (s < logS) v += dpp_any<T>(v, s);
   return v;
-}
-__device__ __forceinline__ int seg_sum32(int v, int S, int smax) {
-  if (smax > 1) { int o = dpp_shl32<0x101>(v); if (S > 1) v += o; }
-  if (smax > 2) { int o = dpp_shl32<0x102>(v); if (S > 2) v += o; }
-  if (smax > 4) { int o = dpp_shl32<0x104>(v); if (S > 4) v += o; }
-  if (smax > 8) { int o = dpp_shl32<0x108>(v); if (S > 8) v += o; }
-  if (smax > 16) { int o = __shfl_down(v, 16); if (S > 16) v += o; }
-  if (smax > 32) { int o = __shfl_down(v, 32); if (S > 32) v += o; }
-  return v;
-}
-// wave-uniform maximum of a small positive per-lane power of two
-__device__ __forceinline__ int wave_max_pow2(int S) {
-  int m = 1;
-  if (__any(S > 1)) m = 2;
-  if (__any(S > 2)) m = 4;
-  if (__any(S > 4)) m = 8;
-  if (__any(S > 8)) m = 16;
-  if (__any(S > 16)) m = 32;
-  if (__any(S > 32)) m = 64;
-  return m;
 }
 
 // ---------------------------------------------------------- filter tap pairs
@@ -281,19 +285,109 @@ __device__ __forceinline__ MvField mv_field(const int* cp, int ncp, int lw, int 
 struct Geo {       // a lane's CU
   int x, y;        // frame position
   int lw, lh, w, h;
-  int predBase;    // first sample of the CU in the LDS prediction buffer
 };
+
+// Hide a value's origin from the optimizer: per-lane geometry is loop-invariant
+// for a whole work item, and hoisting every address derived from it out of the
+// iteration loop would pin ~60 VGPRs; recomputing them per phase is a few adds.
+__device__ __forceinline__ void opaque(int& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void opaque_geo(Geo& g, int& sx, int& sy) {
+  opaque(g.x); opaque(g.y); opaque(g.lw); opaque(g.lh);
+  opaque(g.w); opaque(g.h); opaque(sx); opaque(sy);
+}
+
+
+// Horizontal 6-tap pass of one window row (5 dwords = samples 0..9 of the row
+// in dword order), offset -IF_INTERNAL_OFFS << 2 = -32768, shift 2
+// (aux_functions.cl:1128-1161).  |t| < 2^14, so rows pack into int16 pairs.
+__device__ __forceinline__ void hrow(const unsigned (&D)[5], const uint4& KA, const uint4& KB,
+                                     int (&t)[4]) {
+  t[0] = dot2(D[0], KA.x, dot2(D[1], KA.y, dot2(D[2], KA.z, dot2(D[3], KA.w, -32768)))) >> 2;
+  t[1] = dot2(D[0], KB.x, dot2(D[1], KB.y, dot2(D[2], KB.z, dot2(D[3], KB.w, -32768)))) >> 2;
+  t[2] = dot2(D[1], KA.x, dot2(D[2], KA.y, dot2(D[3], KA.z, dot2(D[4], KA.w, -32768)))) >> 2;
+  t[3] = dot2(D[1], KB.x, dot2(D[2], KB.y, dot2(D[3], KB.z, dot2(D[4], KB.w, -32768)))) >> 2;
+}
+// Vertical pass, streamed: row pair k = (t[2k], t[2k+1]) (pair 4 = (t[8], 0))
+// feeds output row r through tap-pair set G_{r&1}, entry k - (r >> 1)
+// (aux_functions.cl:1182-1223); integer sums, so the order is free.
+__device__ __forceinline__ void vpair(int k, const int (&t0)[4], const int (&t1)[4],
+                                      const uint4& G0, const uint4& G1, int (&acc)[4][4]) {
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const unsigned P = pack16(t0[c], t1[c]);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int m = k - (r >> 1);
+      if (m < 0 || m > 3 || ((r & 1) == 0 && m == 3)) continue;  // set 0 ends with (0,0)
+      const uint4& G = (r & 1) ? G1 : G0;
+      const unsigned g = m == 0 ? G.x : m == 1 ? G.y : m == 2 ? G.z : G.w;
+      acc[r][c] = dot2(P, g, acc[r][c]);
+    }
+  }
+}
+template <int PITCH_DW>
+__device__ __forceinline__ void filter_rows(const unsigned* src, const uint4& KA, const uint4& KB,
+                                            const uint4& G0, const uint4& G1, int (&acc)[4][4]) {
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    int t0[4], t1[4] = {0, 0, 0, 0};
+    unsigned D[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) D[q] = src[(2 * k) * PITCH_DW + q];
+    hrow(D, KA, KB, t0);
+    if (k < 4) {
+#pragma unroll
+      for (int q = 0; q < 5; q++) D[q] = src[(2 * k + 1) * PITCH_DW + q];
+      hrow(D, KA, KB, t1);
+    }
+    vpair(k, t0, t1, G0, G1, acc);
+  }
+}
+// Window leaves the LDS tile: clamp-to-edge loads from the frame
+// (affine.cl:254-326), one row at a time (a rare path, kept register-lean:
+// scalar vertical taps read from the LDS tap table).
+__device__ __forceinline__ void filter_rows_global(const uint16_t* __restrict__ ref, int wx, int wy,
+                                                   int W, int H, const uint4& KA, const uint4& KB,
+                                                   const unsigned* s_coef_dw, int fy,
+                                                   int (&acc)[4][4]) {
+#pragma unroll 1
+  for (int i = 0; i < 9; i++) {
+    const uint16_t* row = ref + (size_t)clampi(wy + i, 0, H - 1) * W;
+    unsigned D[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      const unsigned lo = row[clampi(wx + 2 * q, 0, W - 1)];
+      const unsigned hi = q < 4 ? row[clampi(wx + 2 * q + 1, 0, W - 1)] : 0u;
+      D[q] = lo | (hi << 16);
+    }
+    int t[4];
+    hrow(D, KA, KB, t);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int m = i - r;  // vertical tap of window row i for output row r
+      if (m < 0 || m > 5) continue;
+      const unsigned pr = s_coef_dw[fy * 12 + (m >> 1)];  // set 0: (f0,f1) (f2,f3) (f4,f5)
+      const int cf = (int)(short)(m & 1 ? pr >> 16 : pr & 0xFFFF);
+#pragma unroll
+      for (int c = 0; c < 4; c++) acc[r][c] += t[c] * cf;
+    }
+  }
+}
 
 // One 4x4 sub-block: affine MV (affine.cl:215-252), 9x9 window with
 // clamp-to-edge (affine.cl:254-326), separable 6-tap filter (aux_functions.cl
-// :1096-1239, PROF off), prediction to LDS, SATD against the original
-// (aux_functions.cl:1940-2043).
+// :1096-1239, PROF off), SATD against the original (aux_functions.cl:1940-2043).
+// The prediction stays in registers (P[r] = packed sample pairs of row r) for
+// the gradient step, and so do the original samples (O[r]).
 template <int TILE, int TP>
 __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, const Geo& g,
                                           const uint16_t* s_tile, int tx0, int ty0,
                                           const uint16_t* __restrict__ ref,
                                           const uint16_t* __restrict__ cur, int W, int H,
-                                          uint16_t* s_pred, const uint4* s_coef) {
+                                          const uint4* s_coef, uint2 (&P)[4], uint2 (&O)[4]) {
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+    O[r] = *reinterpret_cast<const uint2*>(cur + (size_t)(g.y + sy + r) * W + g.x + sx);
   const int px = f.spread ? (g.w >> 1) : sx + 2, py = f.spread ? (g.h >> 1) : sy + 2;
   int mx = f.bx + f.hx * px + f.vx * py, my = f.by + f.hy * px + f.vy * py;
   mx = (mx + 64 - (mx >= 0)) >> 7;  // roundMv (aux_functions.cl:38-47)
@@ -306,55 +400,29 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   const int sp = inTile ? (tx & 1) : 0;
   const uint4 KA = s_coef[fx * 3 + sp], KB = s_coef[fx * 3 + sp + 1];
   const uint4 G0 = s_coef[fy * 3 + 0], G1 = s_coef[fy * 3 + 1];
-  int tr[9][4];
+  int acc[4][4];
 #pragma unroll
-  for (int i = 0; i < 9; i++) {
-    unsigned D[5];
-    if (inTile) {
-      const unsigned* src = reinterpret_cast<const unsigned*>(s_tile) + (((ty + i) * TP + tx) >> 1);
+  for (int r = 0; r < 4; r++)
 #pragma unroll
-      for (int k = 0; k < 5; k++) D[k] = src[k];
-    } else {
-      const uint16_t* row = ref + (size_t)clampi(wy + i, 0, H - 1) * W;
-      unsigned w9[10];
-#pragma unroll
-      for (int m = 0; m < 9; m++) w9[m] = row[clampi(wx + m, 0, W - 1)];
-      w9[9] = 0;
-#pragma unroll
-      for (int k = 0; k < 5; k++) D[k] = w9[2 * k] | (w9[2 * k + 1] << 16);
-    }
-    // offset -IF_INTERNAL_OFFS << 2 = -32768, shift 2 (aux_functions.cl:1128-1161)
-    tr[i][0] = dot2(D[0], KA.x, dot2(D[1], KA.y, dot2(D[2], KA.z, dot2(D[3], KA.w, -32768)))) >> 2;
-    tr[i][1] = dot2(D[0], KB.x, dot2(D[1], KB.y, dot2(D[2], KB.z, dot2(D[3], KB.w, -32768)))) >> 2;
-    tr[i][2] = dot2(D[1], KA.x, dot2(D[2], KA.y, dot2(D[3], KA.z, dot2(D[4], KA.w, -32768)))) >> 2;
-    tr[i][3] = dot2(D[1], KB.x, dot2(D[2], KB.y, dot2(D[3], KB.z, dot2(D[4], KB.w, -32768)))) >> 2;
+    for (int c = 0; c < 4; c++) acc[r][c] = 524800;  // (1 << 9) + (8192 << 6)
+  if (inTile) {
+    const unsigned* src = reinterpret_cast<const unsigned*>(s_tile) + ((ty * TP + tx) >> 1);
+    filter_rows<TP / 2>(src, KA, KB, G0, G1, acc);
+  } else {
+    filter_rows_global(ref, wx, wy, W, H, KA, KB, reinterpret_cast<const unsigned*>(s_coef), fy,
+                       acc);
   }
-  // vertical: rows packed in pairs (t[2k], t[2k+1]); offset (1<<9) + (8192<<6),
-  // shift 10, clipPel to [0, 1023] (aux_functions.cl:1182-1223)
   int pr[4][4];
 #pragma unroll
-  for (int c = 0; c < 4; c++) {
-    unsigned P[5];
+  for (int r = 0; r < 4; r++)
 #pragma unroll
-    for (int k = 0; k < 4; k++) P[k] = pack16(tr[2 * k][c], tr[2 * k + 1][c]);
-    P[4] = pack16(tr[8][c], 0);
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const uint4 G = (r & 1) ? G1 : G0;
-      const int b = r >> 1;
-      const int acc =
-          dot2(P[b], G.x, dot2(P[b + 1], G.y, dot2(P[b + 2], G.z, dot2(P[b + 3], G.w, 524800))));
-      pr[r][c] = clampi(acc >> 10, 0, 1023);
-    }
-  }
+    for (int c = 0; c < 4; c++) pr[r][c] = clampi(acc[r][c] >> 10, 0, 1023);  // clipPel
   int diff[16];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
-    uint2 pk;
-    pk.x = pack16(pr[r][0], pr[r][1]);
-    pk.y = pack16(pr[r][2], pr[r][3]);
-    *reinterpret_cast<uint2*>(&s_pred[g.predBase + (sy + r) * g.w + sx]) = pk;
-    const uint2 o = *reinterpret_cast<const uint2*>(cur + (size_t)(g.y + sy + r) * W + g.x + sx);
+    P[r].x = pack16(pr[r][0], pr[r][1]);
+    P[r].y = pack16(pr[r][2], pr[r][3]);
+    const uint2 o = O[r];
     diff[r * 4 + 0] = (int)(o.x & 0xFFFF) - pr[r][0];
     diff[r * 4 + 1] = (int)(o.x >> 16) - pr[r][1];
     diff[r * 4 + 2] = (int)(o.y & 0xFFFF) - pr[r][2];
@@ -389,29 +457,34 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   return (sa + 1) >> 1;
 }
 
+// Extended prediction row of a sub-block: columns -1..4 as the packed pairs
+// (c-1,c0) (c0,c1) (c2,c3) (c3,c4); (c1,c2) is re-derived where needed.
+// Column -1 comes from the left lane's column 3 and column 4 from the right
+// lane's column 0 (DPP wave_shr:1 / wave_shl:1 -- lanes of a CU row are
+// consecutive; at CU edges the values are never used, see grad_sb).
+__device__ __forceinline__ uint4 ext_row(const uint2& p, unsigned left, unsigned right) {
+  return make_uint4(__builtin_amdgcn_alignbit(p.x, left, 16), p.x, p.y,
+                    __builtin_amdgcn_alignbit(right, p.y, 16));
+}
+
 // One 4x4 sub-block of the gradient step (affine.cl:477-708): 3x3 Sobel on the
-// LDS prediction with the CU-border replication of affine.cl:506-540 (rows
-// first, then columns), residual orig - pred (affine.cl:547-579) and the five
+// 6x6 prediction patch (own rows as extended rows X[1..4], the neighbours' edge
+// rows X[0] above and X[5] below) with the CU-border replication of
+// affine.cl:506-540 (rows first, then columns) -- so patch samples outside the
+// CU are never used -- the residual orig - pred (affine.cl:547-579) and the five
 // sums S = (gx.gx, gx.gy, gy.gy, gx.e, gy.e).  Samples are handled as packed
 // int16 pairs: |g| <= 4092 and |e| <= 1023 fit, and v_dot2_i32_i16 sums stay
 // below 2^28 (exact).
-__device__ __forceinline__ void grad_sb(int sx, int sy, const Geo& g,
-                                        const uint16_t* __restrict__ cur, int W,
-                                        const uint16_t* s_pred, int S[5]) {
+__device__ __forceinline__ void grad_sb(int sx, int sy, const Geo& g, const uint4 (&X)[6],
+                                        const uint2 (&Orig)[4], int S[5]) {
   short2v O[6][3], E[6][2];
 #pragma unroll
   for (int i = 0; i < 6; i++) {
-    // prediction row clamped into the CU; dwords cover samples sx-2 .. sx+5.
-    // Samples outside the CU only reach gradients the replication overwrites.
-    const int rr = clampi(sy - 1 + i, 0, g.h - 1);
-    const unsigned* src =
-        reinterpret_cast<const unsigned*>(s_pred) + ((g.predBase + rr * g.w + sx - 2) >> 1);
-    const unsigned D0 = src[0], D1 = src[1], D2 = src[2], D3 = src[3];
-    O[i][0] = as_s2(__builtin_amdgcn_alignbit(D1, D0, 16));  // (sx-1, sx)
-    O[i][1] = as_s2(__builtin_amdgcn_alignbit(D2, D1, 16));  // (sx+1, sx+2)
-    O[i][2] = as_s2(__builtin_amdgcn_alignbit(D3, D2, 16));  // (sx+3, sx+4)
-    E[i][0] = as_s2(D1);                                     // (sx, sx+1)
-    E[i][1] = as_s2(D2);                                     // (sx+2, sx+3)
+    O[i][0] = as_s2(X[i].x);                                      // (sx-1, sx)
+    O[i][1] = as_s2(__builtin_amdgcn_alignbit(X[i].z, X[i].y, 16));  // (sx+1, sx+2)
+    O[i][2] = as_s2(X[i].w);                                      // (sx+3, sx+4)
+    E[i][0] = as_s2(X[i].y);                                      // (sx, sx+1)
+    E[i][1] = as_s2(X[i].z);                                      // (sx+2, sx+3)
   }
   short2v gx[4][2], gy[4][2];
 #pragma unroll
@@ -453,7 +526,7 @@ __device__ __forceinline__ void grad_sb(int sx, int sy, const Geo& g,
   int sxx = 0, sxy = 0, syy = 0, sxe = 0, sye = 0;
 #pragma unroll
   for (int r = 0; r < 4; r++) {
-    const uint2 o = *reinterpret_cast<const uint2*>(cur + (size_t)(g.y + sy + r) * W + g.x + sx);
+    const uint2 o = Orig[r];
     const unsigned e0 = as_u(as_s2(o.x) - E[r + 1][0]), e1 = as_u(as_s2(o.y) - E[r + 1][1]);
     const unsigned x0 = as_u(gx[r][0]), x1 = as_u(gx[r][1]);
     const unsigned y0 = as_u(gy[r][0]), y1 = as_u(gy[r][1]);
@@ -464,42 +537,6 @@ __device__ __forceinline__ void grad_sb(int sx, int sy, const Geo& g,
     sye = dot2(y0, e0, dot2(y1, e1, sye));
   }
   S[0] = sxx; S[1] = sxy; S[2] = syy; S[3] = sxe; S[4] = sye;
-}
-
-// A sub-block's contribution to its CU's normal equations (affine.cl:683-707:
-// every sample of the sub-block uses the sub-block centre (u, v)).
-// 2 CP, iC = (gx, u gx + v gy, gy, v gx - u gy) (affine.cl:691-694): the 10
-// distinct entries of the symmetric matrix, then the 4 right-hand sides.
-__device__ __forceinline__ void values_2cp(const int S[5], long long u, long long v, long long* o) {
-  const long long xx = S[0], xy = S[1], yy = S[2], xe = S[3], ye = S[4];
-  const long long uu = u * u, uv = u * v, vv = v * v;
-  o[0] += xx;                                  // A00
-  o[1] += u * xx + v * xy;                     // A01
-  o[2] += xy;                                  // A02
-  o[3] += v * xx - u * xy;                     // A03
-  o[4] += uu * xx + 2 * uv * xy + vv * yy;     // A11
-  o[5] += u * xy + v * yy;                     // A12
-  o[6] += uv * xx + (vv - uu) * xy - uv * yy;  // A13
-  o[7] += yy;                                  // A22
-  o[8] += v * xy - u * yy;                     // A23
-  o[9] += vv * xx - 2 * uv * xy + uu * yy;     // A33
-  o[10] += xe;                                 // b0
-  o[11] += u * xe + v * ye;                    // b1
-  o[12] += ye;                                 // b2
-  o[13] += v * xe - u * ye;                    // b3
-}
-// 3 CP (affine.cl:684-689): moments {1,u,v,uu,uv,vv} x {xx,xy,yy}, {1,u,v} x {xe,ye}
-__device__ __forceinline__ void values_3cp(const int S[5], long long u, long long v, long long* o) {
-  const long long mono[6] = {1, u, v, u * u, u * v, v * v};
-#pragma unroll
-  for (int s = 0; s < 3; s++)
-#pragma unroll
-    for (int k = 0; k < 6; k++) o[s * 6 + k] += mono[k] * (long long)S[s];
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    o[18 + k] += mono[k] * (long long)S[3];
-    o[21 + k] += mono[k] * (long long)S[4];
-  }
 }
 
 // 3-CP regressors as linear forms in (1, u, v): iC_c = alpha_c . gx + beta_c . gy
@@ -629,45 +666,68 @@ struct CuState {  // 64 bytes
 
 template <int REGION>
 struct Cfg {
-  static constexpr int SBPL = REGION == 128 ? 4 : 1;    // sub-blocks per lane
+  static constexpr int THREADS = REGION == 128 ? 1024 : 256;  // workgroup size = sub-blocks
   static constexpr int TILE = REGION + 2 * kMargin;     // tile edge (samples)
-  static constexpr int TP = REGION == 128 ? 176 : 112;  // tile pitch (samples), == 16 (mod 32)
+  // tile pitch (samples) == 8 (mod 16): the window rows of sub-blocks 4 rows
+  // apart land 16 banks apart (2-way at most for the packed-pair reads)
+  static constexpr int TP = REGION == 128 ? 168 : 104;
   static constexpr int TILE_ELEMS = TILE * TP + 16;
-  static constexpr int PRED_ELEMS = REGION * REGION + 2 * kPredPad + 8;
+  static constexpr int NSB = REGION * REGION / 16;      // sub-blocks per work item (max)
 };
 
-// The reduced equations of this lane's sub-blocks for one CU: leader lanes of
-// each segment store (autonomous) or add (cooperative) into LDS.
-template <int NV, int SBPL, bool THREE>
-__device__ __forceinline__ void gradient_phase(bool active, int localSb0, int lcols, const Geo& g,
-                                               const uint16_t* __restrict__ cur, int W,
-                                               const uint16_t* s_pred, int segS, int segMax,
-                                               bool leader, bool coop, long long* dst) {
-  long long val[NV];
-#pragma unroll
-  for (int i = 0; i < NV; i++) val[i] = 0;
-  if (active && !(VAME_ABLATE & 2)) {
-#pragma unroll 1
-    for (int j = 0; j < SBPL; j++) {
-      const int local = localSb0 + j;
-      const int sx = (local & ((1 << lcols) - 1)) << 2, sy = (local >> lcols) << 2;
-      int S[5];
-      grad_sb(sx, sy, g, cur, W, s_pred, S);
-      if (THREE)
-        values_3cp(S, sx + 2, sy + 2, val);
-      else
-        values_2cp(S, sx + 2, sy + 2, val);
+// Value i of a sub-block's contribution to its CU's normal equations
+// (affine.cl:683-707: every sample of a sub-block uses the sub-block centre
+// (u, v)), from the sub-block's five sums S.
+//   2 CP, iC = (gx, u gx + v gy, gy, v gx - u gy) (affine.cl:691-694): the 10
+//        distinct entries A00 A01 A02 A03 A11 A12 A13 A22 A23 A33 of the
+//        symmetric matrix, then b0..b3 (before the << 3);
+//   3 CP (affine.cl:684-689): the moments {1,u,v,uu,uv,vv} x {xx,xy,yy}, then
+//        {1,u,v} x {xe,ye}; solve_cu forms the matrix from them.
+template <int NCP>
+__device__ __forceinline__ long long eq_value(int i, const int (&S)[5], int u, int v) {
+  const long long xx = S[0], xy = S[1], yy = S[2], xe = S[3], ye = S[4];
+  const long long U = u, V = v;
+  if constexpr (NCP == 2) {
+    switch (i) {
+      case 0: return xx;
+      case 1: return U * xx + V * xy;
+      case 2: return xy;
+      case 3: return V * xx - U * xy;
+      case 4: return (U * U) * xx + (2 * U * V) * xy + (V * V) * yy;
+      case 5: return U * xy + V * yy;
+      case 6: return (U * V) * xx + (V * V - U * U) * xy - (U * V) * yy;
+      case 7: return yy;
+      case 8: return V * xy - U * yy;
+      case 9: return (V * V) * xx - (2 * U * V) * xy + (U * U) * yy;
+      case 10: return xe;
+      case 11: return U * xe + V * ye;
+      case 12: return ye;
+      default: return V * xe - U * ye;
     }
+  } else {
+    const int sidx = i < 18 ? i / 6 : (i < 21 ? 3 : 4);
+    const int mono = i < 18 ? i % 6 : (i - 18) % 3;
+    const long long m = mono == 0 ? 1 : mono == 1 ? U : mono == 2 ? V : mono == 3 ? U * U
+                        : mono == 4 ? U * V : V * V;
+    return m * (long long)S[sidx];
   }
-  if (VAME_ABLATE & 4) return;
+}
+
+// Reduction of a CU's equations over its sub-blocks (one per lane): the last
+// lane of every segment stores (autonomous) or adds (cooperative) the
+// segment's sums into the CU's LDS row.
+template <int NCP>
+__device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v, int logS,
+                                                 bool leader, bool coop, long long* dst) {
+  constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
 #pragma unroll
   for (int i = 0; i < NV; i++) {
-    const long long v = seg_sum64(val[i], segS, segMax);
+    const long long x = seg_sum<long long>(eq_value<NCP>(i, S, u, v), logS);
     if (leader) {
       if (coop)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&dst[i]), (unsigned long long)v);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&dst[i]), (unsigned long long)x);
       else
-        dst[i] = v;
+        dst[i] = x;
     }
   }
 }
@@ -676,14 +736,14 @@ template <int REGION>
 __device__ __forceinline__ void affine_me_body(const KParams& p) {
   using C = Cfg<REGION>;
   __shared__ __attribute__((aligned(16))) uint16_t s_tile[C::TILE_ELEMS];
-  __shared__ __attribute__((aligned(16))) uint16_t s_predBuf[C::PRED_ELEMS];
+  __shared__ uint4 s_top[C::NSB];  // extended row 0 of every sub-block's prediction
+  __shared__ uint4 s_bot[C::NSB];  // extended row 3
   __shared__ __attribute__((aligned(16))) long long s_val[kMaxCu][kNumMom];
   __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
   __shared__ CuState s_st[kMaxCu];
   __shared__ CuSlot s_cu[kMaxCu];
   __shared__ WaveDesc s_wave[kMaxWaves];
   __shared__ int s_hdr[4];
-  uint16_t* s_pred = s_predBuf + kPredPad;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
@@ -707,20 +767,21 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   if (tid < kMaxWaves) s_wave[tid] = it->wave[tid];
   if (tid < 48) s_coef[tid] = reinterpret_cast<const uint4*>(&kCoefTab)[tid];
   if (tid == 0) {
-    s_hdr[0] = it->nCu;
-    s_hdr[1] = it->nWaves | (it->coop << 8);
+    s_hdr[0] = it->nCu | (it->coop << 8) | (it->nWaves << 16) | (it->logL << 24);
     s_hdr[2] = it->rx;
     s_hdr[3] = it->ry;
   }
+  for (int i = tid; i < kMaxCu * kNumMom; i += C::THREADS) (&s_val[0][0])[i] = 0;
   __syncthreads();
-  const int nCu = s_hdr[0], nWaves = s_hdr[1] & 0xFF;
-  const bool coop = (s_hdr[1] >> 8) != 0;
+  const int hdr = __builtin_amdgcn_readfirstlane(s_hdr[0]);
+  const int nCu = hdr & 0xFF, nWaves = (hdr >> 16) & 0xFF;
+  const bool coop = ((hdr >> 8) & 0xFF) != 0;
   const int tx0 = ctuX + s_hdr[2] - kMargin, ty0 = ctuY + s_hdr[3] - kMargin;  // tile origin
 
   // ---- stage the reference region (+margin) into LDS, clamp-to-edge padded
   {
     constexpr int CPR = C::TILE / 4;  // 8-byte chunks per row
-    for (int ch = tid; ch < C::TILE * CPR; ch += kThreads) {
+    for (int ch = tid; ch < C::TILE * CPR; ch += C::THREADS) {
       const int ty = ch / CPR, cx = (ch % CPR) * 4;
       const int fy = clampi(ty0 + ty, 0, H - 1), fx = tx0 + cx;
       const uint16_t* row = ref + (size_t)fy * W;
@@ -736,36 +797,34 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       *reinterpret_cast<uint2*>(&s_tile[ty * C::TP + cx]) = v;
     }
   }
-  if (tid < kMaxCu * kNumMom) (&s_val[0][0])[tid] = 0;
-  if (tid + kThreads < kMaxCu * kNumMom) (&s_val[0][0])[tid + kThreads] = 0;
-  if (tid + 2 * kThreads < kMaxCu * kNumMom) (&s_val[0][0])[tid + 2 * kThreads] = 0;
   __syncthreads();
   if (!coop && wv >= nWaves) return;  // wave-uniform: an autonomous wave without CUs
 
-  // ---- this wave's per-CU lanes, this lane's CU and sub-blocks (fixed per item)
-  int cuB = 0, nCuW = 0, lidx = tid, nSbScope = 0, kEnd = nCu;
+  // ---- CUs of this wave, this lane's CU and sub-blocks (fixed for the item)
+  int cuB, cuE, logL, lidx;
   if (coop) {
-    nCuW = wv == 0 ? nCu : 0;
-    kEnd = nCu;
-    nSbScope = it->nSb;
+    cuB = 0;
+    cuE = nCu;
+    logL = (hdr >> 24) & 0xFF;
+    lidx = tid;
   } else {
     const WaveDesc wd = s_wave[wv];
     cuB = wd.cuBegin;
-    nCuW = wd.cuEnd - wd.cuBegin;
-    kEnd = wd.cuEnd;
-    nSbScope = wd.nSb;
+    cuE = wd.cuEnd;
+    logL = wd.logL;
     lidx = lane;
   }
-  int myCu = -1;
-  if (lidx * C::SBPL < nSbScope) {
-    int k = cuB;
-    for (int j = cuB + 1; j < kEnd; j++)
-      if (s_cu[j].laneBase <= lidx) k = j;
-    myCu = k;
-  }
+  cuB = __builtin_amdgcn_readfirstlane(cuB);
+  cuE = __builtin_amdgcn_readfirstlane(cuE);
+  logL = __builtin_amdgcn_readfirstlane(logL);
+  const int logS = min(logL, 6);                       // segment = lanes of one CU in one wave
+  const int nCuW = coop ? (wv == 0 ? nCu : 0) : cuE - cuB;  // lanes doing per-CU work
+  const int kLane = cuB + (lidx >> logL);
+  const int myCu = kLane < cuE ? kLane : -1;
   Geo g;
-  g.x = g.y = g.lw = g.lh = g.w = g.h = g.predBase = 0;
-  int segS = 1, localSb0 = 0;
+  g.x = g.y = g.lw = g.lh = g.w = g.h = 0;
+  const int local = lidx & ((1 << logL) - 1);  // this lane's sub-block (raster order in its CU)
+  int sbIdx = 0, sx = 0, sy = 0, sbCols = 1;
   bool active = false;
   if (myCu >= 0) {
     const CuSlot cs = s_cu[myCu];
@@ -775,14 +834,14 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     g.h = 1 << g.lh;
     g.x = ctuX + cs.x;
     g.y = ctuY + cs.y;
-    g.predBase = cs.sbBase * 16;
-    segS = min(((g.w * g.h) >> 4) / C::SBPL, 64);
-    localSb0 = (lidx - cs.laneBase) * C::SBPL;
+    sbIdx = cs.sbBase + local;
+    sbCols = 1 << (g.lw - 2);
+    sx = (local & (sbCols - 1)) << 2;
+    sy = (local >> (g.lw - 2)) << 2;
     active = (g.x + g.w <= W) && (g.y + g.h <= H);  // affine.cl:192-193
   }
-  const bool leader = myCu >= 0 && (lane & (segS - 1)) == 0;
-  const int segMax = wave_max_pow2(segS);
-  const int lcols = g.lw - 2;  // log2 of the CU's sub-block columns
+  const int sbTop = max(sbIdx - sbCols, 0), sbBot = min(sbIdx + sbCols, C::NSB - 1);
+  const bool leader = myCu >= 0 && (lane & ((1 << logS) - 1)) == (1 << logS) - 1;
 
   for (int pass = 0; pass < 2; pass++) {
     const int ncp = pass == 0 ? 2 : 3;
@@ -831,20 +890,31 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     for (int iter = 0; iter <= niter; iter++) {
       // =============== prediction + SATD (affine.cl:208-393) ===============
       int satdLane = 0;
+      uint2 Pr[4], Og[4];  // this lane's prediction and original rows (packed pairs)
+#pragma unroll
+      for (int r = 0; r < 4; r++) Pr[r] = Og[r] = make_uint2(0, 0);
       if (active && !(VAME_ABLATE & 8)) {
+        Geo gp = g;
+        int sxp = sx, syp = sy;
+        opaque_geo(gp, sxp, syp);
         int cp[6];
         for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
-        const MvField f = mv_field(cp, ncp, g.lw, g.lh);
-#pragma unroll 1
-        for (int j = 0; j < C::SBPL; j++) {
-          const int local = localSb0 + j;
-          const int sx = (local & ((1 << lcols) - 1)) << 2, sy = (local >> lcols) << 2;
-          satdLane += predict_sb<C::TILE, C::TP>(f, sx, sy, g, s_tile, tx0, ty0, ref, cur, W, H,
-                                                 s_pred, s_coef);
-        }
+        const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
+        satdLane = predict_sb<C::TILE, C::TP>(f, sxp, syp, gp, s_tile, tx0, ty0, ref, cur, W, H,
+                                              s_coef, Pr, Og);
+      }
+      // extended rows (neighbour columns by DPP), edge rows published for the
+      // sub-blocks above and below
+      uint4 X[6];
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        X[r + 1] = ext_row(Pr[r], dpp32<0x138, 0xF>((int)Pr[r].y), dpp32<0x130, 0xF>((int)Pr[r].x));
+      if (myCu >= 0) {
+        s_top[sbIdx] = X[1];
+        s_bot[sbIdx] = X[4];
       }
       {
-        const int v = seg_sum32(satdLane, segS, segMax);
+        const int v = seg_sum<int>(satdLane, logS);
         if (leader) {
           if (coop)
             atomicAdd(&s_st[myCu].satd, v);
@@ -884,13 +954,24 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       if (lastIter) break;  // uniform
 
       // =============== gradients + normal equations (affine.cl:477-752) ===============
-      long long* dst = s_val[myCu < 0 ? 0 : myCu];
-      if (ncp == 2)
-        gradient_phase<kNumVal2, C::SBPL, false>(active, localSb0, lcols, g, cur, W, s_pred, segS,
-                                                 segMax, leader, coop, dst);
-      else
-        gradient_phase<kNumMom, C::SBPL, true>(active, localSb0, lcols, g, cur, W, s_pred, segS,
-                                               segMax, leader, coop, dst);
+      {
+        int S[5] = {0, 0, 0, 0, 0};
+        if (active && !(VAME_ABLATE & 2)) {
+          X[0] = s_bot[sbTop];
+          X[5] = s_top[sbBot];
+          Geo gg = g;
+          int sxg = sx, syg = sy;
+          opaque_geo(gg, sxg, syg);
+          grad_sb(sxg, syg, gg, X, Og, S);
+        }
+        if (!(VAME_ABLATE & 4)) {
+          long long* dst = s_val[myCu < 0 ? 0 : myCu];
+          if (ncp == 2)
+            reduce_equations<2>(S, sx + 2, sy + 2, logS, leader, coop, dst);
+          else
+            reduce_equations<3>(S, sx + 2, sy + 2, logS, leader, coop, dst);
+        }
+      }
       phase_sync(coop);
 
       // =============== solve + CPMV update (affine.cl:782-893), one lane per CU ===============
@@ -933,7 +1014,14 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 }
 
 // Distinct entry points so profiles tell the two work-item classes apart.
-__global__ __launch_bounds__(kThreads) void affine_me_quad(KParams p) { affine_me_body<64>(p); }
-__global__ __launch_bounds__(kThreads) void affine_me_ctu(KParams p) { affine_me_body<128>(p); }
+// Quadrant items: 4 workgroups per CU fit the LDS (~35 KB each), so cap the
+// VGPRs at 128 to let all 16 waves be resident.
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad(
+    KParams p) {
+  affine_me_body<64>(p);
+}
+// 128-class items: one 1024-thread workgroup per CU (94 KB of LDS), one lane
+// per sub-block of a 128x128 CU.
+__global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_body<128>(p); }
 
 }  // namespace vame
