@@ -113,7 +113,7 @@ Item make_auto_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& wave
       if (nsb_of(c) != nsb) abort();
       used += nsb;
     }
-    if (used > 64) abort();
+    if (used > 64 || nsb < 16) abort();  // the kernel's segment sums handle 16 / 32 / 64
     it.wave[w].cuBegin = (int16_t)all.size();
     all.insert(all.end(), waves[w].begin(), waves[w].end());
     it.wave[w].cuEnd = (int16_t)all.size();

@@ -180,51 +180,11 @@ __device__ __forceinline__ int scale_delta(double d) {
   return shl(cvt_i32_f64(d * 4.0 + s * 0.5), 2);
 }
 
-// Segment sums over aligned segments of S lanes (S a power of two <= 64 and
-// UNIFORM across the wave -- the host packs every wave with CUs of one size):
-// the LAST lane of every segment ends with the segment total.  row_shr steps
-// inside a 16-lane DPP row (bound_ctrl: out-of-row sources read 0), then
-// row_bcast:15 / row_bcast:31 across rows (GFX9 DPP).  A segment's last lane
-// only ever adds lanes of its own segment, so no masking is needed.
+// DPP lane shift with zero fill for lanes whose source is outside the pattern
+// (bound_ctrl) or whose row is masked off (old = 0).
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ int dpp32(int v) {
   return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWMASK, 0xF, true);
-}
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ long long dpp64(long long v) {
-  const int lo = dpp32<CTRL, ROWMASK>((int)v);
-  const int hi = dpp32<CTRL, ROWMASK>((int)(v >> 32));
-  return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
-}
-template <typename T>
-__device__ __forceinline__ T dpp_any(T v, int step) {
-  if constexpr (sizeof(T) == 8) {
-    switch (step) {
-      case 0: return dpp64<0x111, 0xF>(v);
-      case 1: return dpp64<0x112, 0xF>(v);
-      case 2: return dpp64<0x114, 0xF>(v);
-      case 3: return dpp64<0x118, 0xF>(v);
-      case 4: return dpp64<0x142, 0xA>(v);
-      default: return dpp64<0x143, 0xC>(v);
-    }
-  } else {
-    switch (step) {
-      case 0: return dpp32<0x111, 0xF>(v);
-      case 1: return dpp32<0x112, 0xF>(v);
-      case 2: return dpp32<0x114, 0xF>(v);
-      case 3: return dpp32<0x118, 0xF>(v);
-      case 4: return dpp32<0x142, 0xA>(v);
-      default: return dpp32<0x143, 0xC>(v);
-    }
-  }
-}
-// logS: log2 of the (wave-uniform, scalar) segment size
-template <typename T>
-__device__ __forceinline__ T seg_sum(T v, int logS) {
-#pragma unroll
-  for (int s = 0; s < 6; s++)
-    if (s < logS) v += dpp_any<T>(v, s);
-  return v;
 }
 
 // ---------------------------------------------------------- filter tap pairs
@@ -713,22 +673,53 @@ __device__ __forceinline__ long long eq_value(int i, const int (&S)[5], int u, i
   }
 }
 
+// Segment sums over aligned segments of 2^LOGS lanes (LOGS <= 6; the host packs
+// every wave with CUs of one size, so the segment size is wave-uniform): the
+// LAST lane of every segment ends with the segment total.  row_shr steps inside
+// a 16-lane DPP row, then row_bcast:15 / row_bcast:31 across rows (GFX9 DPP);
+// a segment's last lane only ever adds lanes of its own segment, so no masking
+// is needed.  One v_add_u32_dpp per step.
+template <int LOGS>
+__device__ __forceinline__ int seg_sum_c(int v) {
+  if (LOGS > 0) v += dpp32<0x111, 0xF>(v);
+  if (LOGS > 1) v += dpp32<0x112, 0xF>(v);
+  if (LOGS > 2) v += dpp32<0x114, 0xF>(v);
+  if (LOGS > 3) v += dpp32<0x118, 0xF>(v);
+  if (LOGS > 4) v += dpp32<0x142, 0xA>(v);
+  if (LOGS > 5) v += dpp32<0x143, 0xC>(v);
+  return v;
+}
+
 // Reduction of a CU's equations over its sub-blocks (one per lane): the last
 // lane of every segment stores (autonomous) or adds (cooperative) the
-// segment's sums into the CU's LDS row.
-template <int NCP>
-__device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v, int logS,
-                                                 bool leader, bool coop, long long* dst) {
+// segment's sums into the CU's LDS row.  Each int64 value x is reduced as two
+// int32 halves, x = hi * 2^24 + lo with lo in [0, 2^24): |x| < 2^44, so over
+// at most 64 lanes sum(lo) < 2^30 and |sum(hi)| < 2^26 -- exact.
+template <int NCP, int LOGS>
+__device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int v, bool leader,
+                                                   bool coop, long long* dst) {
   constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
 #pragma unroll
   for (int i = 0; i < NV; i++) {
-    const long long x = seg_sum<long long>(eq_value<NCP>(i, S, u, v), logS);
+    const long long x = eq_value<NCP>(i, S, u, v);
+    const int lo = seg_sum_c<LOGS>((int)((unsigned)x & 0xFFFFFFu));
+    const int hi = seg_sum_c<LOGS>((int)(x >> 24));
     if (leader) {
+      const long long r = (long long)hi * (1ll << 24) + (long long)(unsigned)lo;
       if (coop)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&dst[i]), (unsigned long long)x);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&dst[i]), (unsigned long long)r);
       else
-        dst[i] = x;
+        dst[i] = r;
     }
+  }
+}
+template <int NCP>
+__device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v, int logS,
+                                                 bool leader, bool coop, long long* dst) {
+  switch (logS) {  // wave-uniform; work items only hold CUs of 16, 32 or >= 64 sub-blocks
+    case 4: reduce_equations_c<NCP, 4>(S, u, v, leader, coop, dst); break;
+    case 5: reduce_equations_c<NCP, 5>(S, u, v, leader, coop, dst); break;
+    default: reduce_equations_c<NCP, 6>(S, u, v, leader, coop, dst); break;
   }
 }
 
@@ -914,7 +905,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         s_bot[sbIdx] = X[4];
       }
       {
-        const int v = seg_sum<int>(satdLane, logS);
+        const int v = logS == 4 ? seg_sum_c<4>(satdLane)
+                      : logS == 5 ? seg_sum_c<5>(satdLane) : seg_sum_c<6>(satdLane);
         if (leader) {
           if (coop)
             atomicAdd(&s_st[myCu].satd, v);
