@@ -499,65 +499,92 @@ __device__ __forceinline__ void grad_sb(int sx, int sy, const Geo& g, const uint
   S[0] = sxx; S[1] = sxy; S[2] = syy; S[3] = sxe; S[4] = sye;
 }
 
-// 3-CP regressors as linear forms in (1, u, v): iC_c = alpha_c . gx + beta_c . gy
-// (gx, u gx, gy, u gy, v gx, v gy); product of two forms against the moments.
-__device__ __forceinline__ long long qf(const int* p, const int* q, const long long* m) {
-  return (long long)(p[0] * q[0]) * m[0] + (long long)(p[0] * q[1] + p[1] * q[0]) * m[1] +
-         (long long)(p[0] * q[2] + p[2] * q[0]) * m[2] + (long long)(p[1] * q[1]) * m[3] +
-         (long long)(p[1] * q[2] + p[2] * q[1]) * m[4] + (long long)(p[2] * q[2]) * m[5];
+// Element (r, c) of a CU's normal equations (affine.cl:759-763) from its
+// reduced values V; column N is the right-hand side (<< 3, affine.cl:705).
+// Integer sums below 2^53 convert to double exactly.
+template <int NCP>
+__device__ __forceinline__ double eq_element(const long long* V, int r, int c) {
+  if constexpr (NCP == 2) {
+    if (c == 4) return (double)(V[10 + r] * 8);
+    const int lo = min(r, c), hi = max(r, c);  // symmetric: A00 A01 A02 A03 A11 A12 A13 A22 A23 A33
+    return (double)V[lo == 0 ? hi : lo == 1 ? 3 + hi : lo == 2 ? 5 + hi : 9];
+  } else {
+    // regressor r = (gradient t: 0 x / 1 y, monomial m: 0 1 / 1 u / 2 v):
+    // gx, u gx, gy, u gy, v gx, v gy (affine.cl:684-689)
+    const int tr = (r == 2 || r == 3 || r == 5) ? 1 : 0, mr = (r == 1 || r == 3) ? 1 : (r >= 4 ? 2 : 0);
+    if (c == 6) return (double)(V[18 + 3 * tr + mr] * 8);
+    const int tc = (c == 2 || c == 3 || c == 5) ? 1 : 0, mc = (c == 1 || c == 3) ? 1 : (c >= 4 ? 2 : 0);
+    const int prod = mr == 0 ? mc : mc == 0 ? mr : (mr == 1 && mc == 1) ? 3 : (mr == 2 && mc == 2) ? 5 : 4;
+    return (double)V[6 * (tr + tc) + prod];
+  }
 }
 
-// VTM solveEqual (affine.cl:782-856) on R[r] = private_dEqualCoeff[r + 1]
-// (affine.cl:759-763), all indices static so the system stays in registers:
-// pivot search with the sequential strict-'>' scan (NaN never wins), row swap,
-// elimination a[j][k] -= a[i][k] * a[j][i-1] / a[i][i-1] (no zero-pivot guard),
-// back-substitution with fma (FP_CONTRACT) and the zero-pivot reset.
+// VTM solveEqual (affine.cl:782-856), forward elimination shared by the lanes
+// of a CU's segment (li = lane in the segment, Ls = segment size) on the CU's
+// matrix M (row r = private_dEqualCoeff[r + 1], N + 1 columns) in LDS:
+// every lane repeats the pivot search (sequential strict '>' scan, NaN never
+// wins); the row swap and then each element a[j][k] -= a[i][k] * a[j][i-1] /
+// a[i][i-1] of the step (no zero-pivot guard) is done by one lane, with the
+// reference's operation order.  Columns left of the pivot are dead and skipped.
+// Called by every lane of the wave (act: lane works on a live CU).
 template <int N>
-__device__ __forceinline__ void solve_equal(double (&R)[N][N + 1], double (&p)[N]) {
+__device__ __forceinline__ void seg_eliminate(double* M, int li, int Ls, bool act) {
+  constexpr int NC = N + 1;
 #pragma unroll
   for (int i = 1; i < N; i++) {
-    double temp = fabs(R[i - 1][i - 1]);
-    int idx = i - 1;
+    if (act) {
+      double temp = fabs(M[(i - 1) * NC + i - 1]);
+      int idx = i - 1;
 #pragma unroll
-    for (int r = i; r < N; r++) {
-      const double f = fabs(R[r][i - 1]);
-      if (f > temp) {
-        temp = f;
-        idx = r;
+      for (int r = i; r < N; r++) {
+        const double f = fabs(M[r * NC + i - 1]);
+        if (f > temp) {
+          temp = f;
+          idx = r;
+        }
+      }
+      if (idx != i - 1 && li < N + 2 - i) {
+        const int c = i - 1 + li;
+        const double a = M[(i - 1) * NC + c], b = M[idx * NC + c];
+        M[(i - 1) * NC + c] = b;
+        M[idx * NC + c] = a;
       }
     }
-#pragma unroll
-    for (int r = i; r < N; r++) {
-      const bool sw = idx == r;
-#pragma unroll
-      for (int c = 0; c <= N; c++) {
-        const double a = R[i - 1][c], b = R[r][c];
-        R[i - 1][c] = sw ? b : a;
-        R[r][c] = sw ? a : b;
+    wave_sync();
+    const int cols = N + 1 - i, E = (N - i) * cols;  // constants after unrolling
+    if (act) {
+      for (int e = li; e < E; e += Ls) {
+        const int r = i + e / cols, k = i + e % cols;
+        M[r * NC + k] = __dsub_rn(M[r * NC + k], __ddiv_rn(__dmul_rn(M[(i - 1) * NC + k], M[r * NC + i - 1]),
+                                                           M[(i - 1) * NC + i - 1]));
       }
     }
-#pragma unroll
-    for (int r = i; r < N; r++) {
-      const double f = R[r][i - 1];
-#pragma unroll
-      for (int k = i; k <= N; k++)
-        R[r][k] = __dsub_rn(R[r][k], __ddiv_rn(__dmul_rn(R[i - 1][k], f), R[i - 1][i - 1]));
-    }
+    wave_sync();
   }
+}
+
+// Back-substitution of solveEqual (affine.cl:832-856): fma where the
+// reference's FP_CONTRACT fuses, all-zero result on a zero pivot; then the
+// deltas fed to scaleDeltaMvs (affine.cl:860-883).
+template <int NCP>
+__device__ __forceinline__ void back_substitute(const double* M, int lw, int lh, double dd[6]) {
+  constexpr int N = 2 * NCP, NC = N + 1;
+  double p[N];
 #pragma unroll
   for (int k = 0; k < N; k++) p[k] = 0.;
-  p[N - 1] = __ddiv_rn(R[N - 1][N], R[N - 1][N - 1]);
+  p[N - 1] = __ddiv_rn(M[(N - 1) * NC + N], M[(N - 1) * NC + N - 1]);
   bool zero = false;
 #pragma unroll
   for (int i = N - 2; i >= 0; i--) {
     if (!zero) {
-      if (R[i][i] == 0.) {
+      const double piv = M[i * NC + i];
+      if (piv == 0.) {
         zero = true;
       } else {
         double temp = 0;
 #pragma unroll
-        for (int j = i + 1; j < N; j++) temp = fma(R[i][j], p[j], temp);
-        p[i] = __ddiv_rn(__dsub_rn(R[i][N], temp), R[i][i]);
+        for (int j = i + 1; j < N; j++) temp = fma(M[i * NC + j], p[j], temp);
+        p[i] = __ddiv_rn(__dsub_rn(M[i * NC + N], temp), piv);
       }
     }
   }
@@ -565,42 +592,6 @@ __device__ __forceinline__ void solve_equal(double (&R)[N][N + 1], double (&p)[N
 #pragma unroll
     for (int k = 0; k < N; k++) p[k] = 0.;
   }
-}
-
-// One CU's equations (reduced values V) -> the deltas fed to scaleDeltaMvs
-// (affine.cl:860-883).
-template <int NCP>
-__device__ __forceinline__ void solve_cu(const long long* V, int lw, int lh, double dd[6]) {
-  constexpr int N = 2 * NCP;
-  double R[N][N + 1];
-  if constexpr (NCP == 2) {
-    const long long A[4][4] = {{V[0], V[1], V[2], V[3]},
-                               {V[1], V[4], V[5], V[6]},
-                               {V[2], V[5], V[7], V[8]},
-                               {V[3], V[6], V[8], V[9]}};
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-#pragma unroll
-      for (int r = 0; r < 4; r++) R[c][r] = (double)A[c][r];
-      R[c][4] = (double)(V[10 + c] * 8);  // rhs << 3 (affine.cl:705)
-    }
-  } else {
-    constexpr int al[6][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1}, {0, 0, 0}};
-    constexpr int be[6][3] = {{0, 0, 0}, {0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 0}, {0, 0, 1}};
-#pragma unroll
-    for (int c = 0; c < 6; c++) {
-#pragma unroll
-      for (int r = 0; r < 6; r++)
-        R[c][r] = (double)(qf(al[c], al[r], V + 0) + qf(al[c], be[r], V + 6) +
-                           qf(be[c], al[r], V + 6) + qf(be[c], be[r], V + 12));
-      long long b = 0;
-#pragma unroll
-      for (int k = 0; k < 3; k++) b += (long long)al[c][k] * V[18 + k] + (long long)be[c][k] * V[21 + k];
-      R[c][6] = (double)(b * 8);
-    }
-  }
-  double p[N];
-  solve_equal<N>(R, p);
   const double w = (double)(1 << lw), h = (double)(1 << lh);
   dd[0] = p[0];
   dd[2] = p[2];
@@ -613,6 +604,21 @@ __device__ __forceinline__ void solve_cu(const long long* V, int lw, int lh, dou
     dd[3] = __dadd_rn(__dmul_rn(-p[3], w), p[2]);
     dd[4] = dd[5] = 0.;
   }
+}
+
+// Build, eliminate and back-substitute one CU's system with its segment; the
+// segment's first lane returns the deltas.
+template <int NCP>
+__device__ __forceinline__ void seg_solve(long long* V, double* M, int li, int Ls, bool act,
+                                          bool coop, int lw, int lh, double dd[6]) {
+  constexpr int N = 2 * NCP, NC = N + 1;
+  if (act) {
+    for (int e = li; e < N * NC; e += Ls) M[e] = eq_element<NCP>(V, e / NC, e % NC);
+    if (coop && li < kNumMom) V[li] = 0;  // cooperative items accumulate with atomics
+  }
+  wave_sync();
+  seg_eliminate<N>(M, li, Ls, act);
+  if (act && li == 0) back_substitute<NCP>(M, lw, lh, dd);
 }
 
 struct CuState {  // 64 bytes
@@ -730,6 +736,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   __shared__ uint4 s_top[C::NSB];  // extended row 0 of every sub-block's prediction
   __shared__ uint4 s_bot[C::NSB];  // extended row 3
   __shared__ __attribute__((aligned(16))) long long s_val[kMaxCu][kNumMom];
+  __shared__ double s_mat[kMaxCu][42];  // per CU: N x (N + 1) system, N <= 6
   __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
   __shared__ CuState s_st[kMaxCu];
   __shared__ CuSlot s_cu[kMaxCu];
@@ -966,21 +973,22 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       }
       phase_sync(coop);
 
-      // =============== solve + CPMV update (affine.cl:782-893), one lane per CU ===============
-      if (lane < nCuW && !(VAME_ABLATE & 1)) {
-        const int k = cuB + lane;
-        CuState& st = s_st[k];
-        if (st.inframe) {
-          const CuSlot cs = s_cu[k];
-          double dd[6];
-          if (ncp == 3)
-            solve_cu<3>(s_val[k], cs.lw, cs.lh, dd);
-          else
-            solve_cu<2>(s_val[k], cs.lw, cs.lh, dd);
-          if (coop) {
-#pragma unroll
-            for (int i = 0; i < kNumMom; i++) s_val[k][i] = 0;
-          }
+      // =============== solve + CPMV update (affine.cl:782-893), per CU segment ===============
+      if (!(VAME_ABLATE & 1)) {
+        // the CU's lanes in its first wave solve it together
+        const bool solver = myCu >= 0 && local < 64;
+        const bool act = solver && s_st[myCu].inframe;
+        const int Ls = 1 << logS;
+        double dd[6] = {0, 0, 0, 0, 0, 0};
+        long long* V = s_val[myCu < 0 ? 0 : myCu];
+        double* M = s_mat[myCu < 0 ? 0 : myCu];
+        if (ncp == 3)
+          seg_solve<3>(V, M, local, Ls, act, coop, g.lw, g.lh, dd);
+        else
+          seg_solve<2>(V, M, local, Ls, act, coop, g.lw, g.lh, dd);
+        if (act && local == 0) {
+          CuState& st = s_st[myCu];
+          const CuSlot cs = s_cu[myCu];
           // affine.cl:884-893 (scaleDeltaMvs order: LT=(d0,d2), RT=(d1,d3), LB=(d4,d5))
           int c6[6];
           c6[0] = (int)((unsigned)st.cur[0] + (unsigned)scale_delta(dd[0]));
