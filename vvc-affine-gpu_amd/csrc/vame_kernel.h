@@ -285,22 +285,33 @@ __device__ __forceinline__ void vpair(int k, const int (&t0)[4], const int (&t1)
     }
   }
 }
+// Window rows from the LDS tile, software-pipelined one row pair ahead (the
+// scheduling barriers keep the compiler from hoisting all 45 reads, which
+// would cost ~40 VGPRs of occupancy).
 template <int PITCH_DW>
 __device__ __forceinline__ void filter_rows(const unsigned* src, const uint4& KA, const uint4& KB,
                                             const uint4& G0, const uint4& G1, int (&acc)[4][4]) {
+  unsigned D[2][2][5];
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+#pragma unroll
+    for (int q = 0; q < 5; q++) D[0][h][q] = src[h * PITCH_DW + q];
 #pragma unroll
   for (int k = 0; k < 5; k++) {
-    int t0[4], t1[4] = {0, 0, 0, 0};
-    unsigned D[5];
+    const int cb = k & 1, nb = cb ^ 1;
+    if (k < 4) {  // prefetch row pair k + 1 (row 9 does not exist)
 #pragma unroll
-    for (int q = 0; q < 5; q++) D[q] = src[(2 * k) * PITCH_DW + q];
-    hrow(D, KA, KB, t0);
-    if (k < 4) {
+      for (int h = 0; h < 2; h++)
+        if (2 * (k + 1) + h < 9) {
 #pragma unroll
-      for (int q = 0; q < 5; q++) D[q] = src[(2 * k + 1) * PITCH_DW + q];
-      hrow(D, KA, KB, t1);
+          for (int q = 0; q < 5; q++) D[nb][h][q] = src[(2 * (k + 1) + h) * PITCH_DW + q];
+        }
     }
+    int t0[4], t1[4] = {0, 0, 0, 0};
+    hrow(D[cb][0], KA, KB, t0);
+    if (k < 4) hrow(D[cb][1], KA, KB, t1);
     vpair(k, t0, t1, G0, G1, acc);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 // Window leaves the LDS tile: clamp-to-edge loads from the frame
@@ -976,19 +987,22 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       // =============== solve + CPMV update (affine.cl:782-893), per CU segment ===============
       if (!(VAME_ABLATE & 1)) {
         // the CU's lanes in its first wave solve it together
-        const bool solver = myCu >= 0 && local < 64;
-        const bool act = solver && s_st[myCu].inframe;
+        int cuS = myCu, loc = local;
+        opaque(cuS);
+        opaque(loc);
+        const bool solver = cuS >= 0 && loc < 64;
+        const bool act = solver && s_st[cuS].inframe;
         const int Ls = 1 << logS;
         double dd[6] = {0, 0, 0, 0, 0, 0};
-        long long* V = s_val[myCu < 0 ? 0 : myCu];
-        double* M = s_mat[myCu < 0 ? 0 : myCu];
+        long long* V = s_val[cuS < 0 ? 0 : cuS];
+        double* M = s_mat[cuS < 0 ? 0 : cuS];
+        const CuSlot cs = s_cu[cuS < 0 ? 0 : cuS];
         if (ncp == 3)
-          seg_solve<3>(V, M, local, Ls, act, coop, g.lw, g.lh, dd);
+          seg_solve<3>(V, M, loc, Ls, act, coop, cs.lw, cs.lh, dd);
         else
-          seg_solve<2>(V, M, local, Ls, act, coop, g.lw, g.lh, dd);
-        if (act && local == 0) {
-          CuState& st = s_st[myCu];
-          const CuSlot cs = s_cu[myCu];
+          seg_solve<2>(V, M, loc, Ls, act, coop, cs.lw, cs.lh, dd);
+        if (act && loc == 0) {
+          CuState& st = s_st[cuS];
           // affine.cl:884-893 (scaleDeltaMvs order: LT=(d0,d2), RT=(d1,d3), LB=(d4,d5))
           int c6[6];
           c6[0] = (int)((unsigned)st.cur[0] + (unsigned)scale_delta(dd[0]));
