@@ -63,14 +63,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
+        # one rank per GPU; VAME_DIST_BACKEND=gloo rehearses the multi-rank path
+        # with several ranks on one GPU (the driver's runs use RCCL)
+        backend = os.environ.get("VAME_DIST_BACKEND", "nccl")
+        local = local % torch.cuda.device_count() if backend != "nccl" else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         dist = None
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from vame import synth
+    from vame import shard, synth
     from vame.engine import Engine
     from vame.hostlogic import lambda_for_poc, ref_list
     from vame.metrics import pair_accounting
@@ -93,25 +100,14 @@ def main():
     acc = pair_accounting(W, H, ncps)
     rows_per_step = n_pairs * acc["rows"]
 
-    gather_src = gather_dst = None
-    if dist is not None:
-        nbytes = sum(c.numel() * 8 + p.numel() * 4 for pl in plan for (c, p) in pl[3].values())
-        gather_src = torch.empty(nbytes // 4, dtype=torch.int32, device=dev)
-        gather_dst = torch.empty(world * gather_src.numel(), dtype=torch.int32, device=dev)
+    layout = [(len(refs), modes, (eng.n_cus(0), eng.n_cus(1))) for (_, refs, _, _) in plan]
+    words = shard.slab_words(layout)
 
     def step():
         for (poc, refs, lam, out) in plan:
             eng.affine_me_poc(d_orig[poc - 1], [d_recon[r] for r in refs], lam, modes, 0, out=out)
-        if dist is not None:  # decision-log gather over RCCL/xGMI
-            ofs = 0
-            for (_, _, _, out) in plan:
-                for (c, p) in out.values():
-                    n = c.numel() * 2
-                    gather_src[ofs:ofs + n].copy_(c.view(torch.int32))
-                    ofs += n
-                    gather_src[ofs:ofs + p.numel()].copy_(p.view(-1))
-                    ofs += p.numel()
-            dist.all_gather_into_tensor(gather_dst, gather_src)
+        if dist is not None:  # the one exchange step: decision-log gather over RCCL/xGMI
+            shard.gather(shard.pack([pl[3] for pl in plan], words, dev), world)
 
     def barrier():
         torch.cuda.synchronize()

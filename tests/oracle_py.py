@@ -83,3 +83,15 @@ def affine_me_pair(ref, cur, lam, extra=0, modes=(2, 3), nthreads=0):
             out[(align, 3)] = affine_me(ref, cur, lam, align, 3, extra, prev=p2,
                                         nthreads=nthreads)
     return out
+
+
+def group_geometry(align):
+    """[(w, h, xs, ys, stride)] per CU group of an alignment, from the oracle's tables."""
+    out = []
+    for g in range(24 if align else 12):
+        w, h, n, s = (np.zeros(1, np.int32) for _ in range(4))
+        xs, ys = np.zeros(64, np.int32), np.zeros(64, np.int32)
+        assert lib().vame_oracle_group_geometry(align, g, ptr(w), ptr(h), ptr(n),
+                                                ptr(s), ptr(xs), ptr(ys)) == 0
+        out.append((int(w[0]), int(h[0]), xs[:n[0]].copy(), ys[:n[0]].copy(), int(s[0])))
+    return out

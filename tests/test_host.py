@@ -1,0 +1,86 @@
+"""CPU tests of the host side: the C ABI library loads and exports every
+symbol include/vame.h declares, the per-POC host logic (lambda, QP, reference
+ring) against tests/golden/hostlogic.json, the product geometry against the
+oracle, and the work accounting of SURVEY.md §8."""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from vame import _lib
+from vame.hostlogic import geometry, lambda_for_poc, poc_qp, ref_list
+from vame.metrics import pair_accounting
+
+import oracle_py as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = json.load(open(os.path.join(REPO, "tests", "golden", "hostlogic.json")))
+
+
+def header_symbols():
+    src = open(os.path.join(REPO, "include", "vame.h")).read()
+    src = re.sub(r"/\*.*?\*/|//[^\n]*", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vame_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 16
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(_lib.EXPORTS) == syms
+
+
+def test_version_and_errors():
+    L = _lib.lib()
+    assert b"gfx950" in L.vame_version()
+    for code in (0, -1, -2, -3, -4):
+        assert L.vame_strerror(code)
+    # no device work: bad arguments fail before touching HIP
+    assert L.vame_affine_me(None, None, None, 1.0, 0, 2, 0, None, None, None, None) == -1
+    assert L.vame_num_ctus(1920, 1080) == 135
+    assert L.vame_num_ctus(3840, 2160) == 510
+    assert L.vame_cus_per_ctu(0) == 201 and L.vame_cus_per_ctu(1) == 284
+
+
+@pytest.mark.parametrize("row", GOLD["lambda"], ids=lambda r: f"qp{r['qp']}_poc{r['poc']}")
+def test_lambda_and_qp(row):
+    assert poc_qp(row["qp"], row["poc"]) == row["poc_qp"]
+    assert np.float32(lambda_for_poc(row["qp"], row["poc"])) == np.float32(row["lambda"])
+
+
+def test_lambda_kats():
+    # SURVEY.md §8a T14
+    assert abs(lambda_for_poc(32, 1) - 78.949063) < 1e-5
+    assert abs(lambda_for_poc(32, 2) - 70.335619) < 1e-5
+    assert abs(lambda_for_poc(32, 8) - 35.167810) < 1e-5
+
+
+def test_reference_ring():
+    for poc, refs in GOLD["ref_lists"].items():
+        assert ref_list(int(poc)) == refs, poc
+
+
+def test_geometry_matches_oracle():
+    for align in (0, 1):
+        prod = geometry(align)
+        ref = O.group_geometry(align)
+        assert len(prod) == len(ref)
+        for (w, h, xs, ys, s), (w2, h2, xs2, ys2, s2) in zip(prod, ref):
+            assert (w, h, s) == (w2, h2, s2)
+            assert (xs == xs2).all() and (ys == ys2).all()
+
+
+def test_pair_accounting_matches_survey():
+    a = pair_accounting(1920, 1080, (2,))
+    assert a["rows"] == 65475 and a["rows_inframe"] == 60810
+    assert a["bytes"] == 2674603500
+    b = pair_accounting(1920, 1080, (2, 3))
+    assert b["bytes"] == 4918027800
+    c = pair_accounting(3840, 2160, (2,))
+    assert c["bytes"] == 10811623320
+    assert pair_accounting(3840, 2160, (2, 3))["bytes"] == 19880178480

@@ -120,15 +120,7 @@ def test_kat3_out_of_frame_rows():
     assert n_out > 0
 
 
-def group_geometry(align):
-    out = []
-    for g in range(24 if align else 12):
-        w, h, n, s = (np.zeros(1, np.int32) for _ in range(4))
-        xs, ys = np.zeros(64, np.int32), np.zeros(64, np.int32)
-        assert O.lib().vame_oracle_group_geometry(align, g, O.ptr(w), O.ptr(h), O.ptr(n),
-                                                  O.ptr(s), O.ptr(xs), O.ptr(ys)) == 0
-        out.append((int(w[0]), int(h[0]), xs[:n[0]].copy(), ys[:n[0]].copy(), int(s[0])))
-    return out
+group_geometry = O.group_geometry
 
 
 @pytest.mark.parametrize("align,total", [(0, 201), (1, 284)])

@@ -1,0 +1,104 @@
+"""Frame-shard multi-GPU plumbing.
+
+The hot path shards by POC: a (POC, ref) pair needs only orig[POC] and the
+recon frames named by the deterministic reference ring (main.cpp:591-707,
+replayed by `hostlogic.ref_list` on every rank), and no result feeds another
+POC.  So every rank codes a contiguous block of POCs with no collective on the
+data path; the only exchange is the decision-log gather at the end (one
+all_gather of equal-size padded int32 slabs, RCCL over xGMI on the GPU box,
+gloo in the CPU tests).
+
+Decision records travel as int32 words: per (POC, ref, mode) the int64 costs
+(2 words each) followed by the [n, 7] Cpmvs words (typedef.h Cpmvs layout).
+"""
+from __future__ import annotations
+
+import torch
+
+MODES = ("FULL_2CP", "FULL_3CP", "HALF_2CP", "HALF_3CP")
+
+
+def pairs_per_poc(poc: int) -> int:
+    """numRefs = min(4, POC) (main.cpp:584)."""
+    return min(4, poc)
+
+
+def poc_shard(n_frames: int, world: int, rank: int) -> list[int]:
+    """Contiguous block of POCs 1..n_frames for `rank`, balanced by pair count
+    (POC 1-3 carry fewer references).  Blocks cover every POC exactly once."""
+    pocs = list(range(1, n_frames + 1))
+    prefix = [0]
+    for p in pocs:
+        prefix.append(prefix[-1] + pairs_per_poc(p))
+    total = prefix[-1]
+    bounds = [0]
+    for r in range(1, world):  # cut nearest to r/world of the pairs, never going back
+        target = r * total / world
+        i = min(range(bounds[-1], len(pocs) + 1), key=lambda j: (abs(prefix[j] - target), j))
+        bounds.append(i)
+    bounds.append(len(pocs))
+    return pocs[bounds[rank]:bounds[rank + 1]]
+
+
+def result_keys(nrefs: int, modes: int):
+    """(refIdx, MODE) keys of one POC's results, in the fixed wire order."""
+    keys = []
+    for r in range(nrefs):
+        for m, name in enumerate(MODES):
+            if (m & 1) and not (modes & 2):
+                continue
+            keys.append((r, name))
+    return keys
+
+
+def pack(results: list[dict], words: int | None = None, device=None) -> torch.Tensor:
+    """Concatenate the results of several POCs ({(ref, MODE): (cost int64[n],
+    cpmv int32[n, 7])}, in POC order) into one int32 slab, zero padded to
+    `words`."""
+    parts = []
+    for res in results:
+        for key in sorted(res, key=lambda k: (k[0], MODES.index(k[1]))):
+            cost, cpmv = res[key]
+            parts.append(cost.reshape(-1).contiguous().view(torch.int32))
+            parts.append(cpmv.reshape(-1).to(torch.int32))
+    flat = torch.cat(parts) if parts else torch.empty(0, dtype=torch.int32, device=device)
+    if words is not None:
+        if flat.numel() > words:
+            raise ValueError("slab larger than the agreed size")
+        flat = torch.cat([flat, flat.new_zeros(words - flat.numel())])
+    return flat
+
+
+def unpack(flat: torch.Tensor, layout: list[tuple[int, int, int]]) -> list[dict]:
+    """Inverse of `pack` for a list of (nrefs, modes, n_cus_per_align) POCs:
+    n_cus_per_align = (FULL rows, HALF rows) of one frame."""
+    out, ofs = [], 0
+    for nrefs, modes, (n_full, n_half) in layout:
+        res = {}
+        for key in result_keys(nrefs, modes):
+            n = n_half if key[1].startswith("HALF") else n_full
+            cost = flat[ofs:ofs + 2 * n].contiguous().view(torch.int64)
+            ofs += 2 * n
+            cpmv = flat[ofs:ofs + 7 * n].view(n, 7)
+            ofs += 7 * n
+            res[key] = (cost, cpmv)
+        out.append(res)
+    return out
+
+
+def slab_words(layout: list[tuple[int, int, int]]) -> int:
+    w = 0
+    for nrefs, modes, (n_full, n_half) in layout:
+        for key in result_keys(nrefs, modes):
+            w += 9 * (n_half if key[1].startswith("HALF") else n_full)
+    return w
+
+
+def gather(slab: torch.Tensor, world: int, group=None) -> list[torch.Tensor]:
+    """The one exchange step: every rank's slab to every rank (equal sizes)."""
+    import torch.distributed as dist
+    if world == 1:
+        return [slab]
+    dst = [torch.empty_like(slab) for _ in range(world)]
+    dist.all_gather(dst, slab, group=group)
+    return dst
