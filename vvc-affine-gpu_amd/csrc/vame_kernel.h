@@ -632,13 +632,18 @@ __device__ __forceinline__ void seg_solve(long long* V, double* M, int li, int L
   if (act && li == 0) back_substitute<NCP>(M, lw, lh, dd);
 }
 
+// Per-CU refinement state.  `live` drops to 0 when the CU is out of frame or
+// when an update leaves its CPMVs unchanged: every later iteration would then
+// repeat the same prediction and cost (never strictly better) and the same
+// zero update, so skipping them leaves the result bit-identical.
 struct CuState {  // 64 bytes
   int32_t cur[6];
   int32_t best[6];
   int64_t bestCost;
   int32_t satd;
   int32_t inframe;
-  int32_t pad[2];
+  int32_t live;
+  int32_t pad;
 };
 
 template <int REGION>
@@ -893,6 +898,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       st.bestCost = kCostInit;
       st.satd = 0;
       st.inframe = (cx + (1 << cs.lw) <= W) && (cy + (1 << cs.lh) <= H);
+      st.live = st.inframe;
     }
     phase_sync(coop);
 
@@ -902,7 +908,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       uint2 Pr[4], Og[4];  // this lane's prediction and original rows (packed pairs)
 #pragma unroll
       for (int r = 0; r < 4; r++) Pr[r] = Og[r] = make_uint2(0, 0);
-      if (active && !(VAME_ABLATE & 8)) {
+      const bool live = active && s_st[myCu < 0 ? 0 : myCu].live;
+      if (live && !(VAME_ABLATE & 8)) {
         Geo gp = g;
         int sxp = sx, syp = sy;
         opaque_geo(gp, sxp, syp);
@@ -939,7 +946,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       if (lane < nCuW) {
         const int k = cuB + lane;
         CuState& st = s_st[k];
-        if (iter == 0 || st.inframe) {
+        if (iter == 0 || st.live) {
           const int bits = affine_bits(st.cur, ncp) + kRuiBits;
           const float prod = __fmul_rn(p.lambda, (float)bits);
           const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
@@ -949,24 +956,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           }
         }
         st.satd = 0;
-        if (lastIter) {  // affine.cl:928-957
-          const CuSlot cs = s_cu[k];
-          const int mode = cs.align * 2 + (ncp - 2);
-          const size_t idx = (size_t)ctu * (cs.align ? kHalfCusPerCtu : kFullCusPerCtu) + cs.outOff;
-          p.cost[refIdx][mode][idx] = st.bestCost;
-          vame_cpmvs_dev o;
-          o.ncps = ncp;
-          o.ltx = st.best[0]; o.lty = st.best[1]; o.rtx = st.best[2];
-          o.rty = st.best[3]; o.lbx = st.best[4]; o.lby = st.best[5];
-          p.cpmv[refIdx][mode][idx] = o;
-        }
       }
       if (lastIter) break;  // uniform
 
       // =============== gradients + normal equations (affine.cl:477-752) ===============
       {
         int S[5] = {0, 0, 0, 0, 0};
-        if (active && !(VAME_ABLATE & 2)) {
+        if (live && !(VAME_ABLATE & 2)) {
           X[0] = s_bot[sbTop];
           X[5] = s_top[sbBot];
           Geo gg = g;
@@ -991,7 +987,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         opaque(cuS);
         opaque(loc);
         const bool solver = cuS >= 0 && loc < 64;
-        const bool act = solver && s_st[cuS].inframe;
+        const bool act = solver && s_st[cuS].live;
         const int Ls = 1 << logS;
         double dd[6] = {0, 0, 0, 0, 0, 0};
         long long* V = s_val[cuS < 0 ? 0 : cuS];
@@ -1017,11 +1013,34 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           clip_mv(c6[0], c6[1], cx, cy, W, H);
           clip_mv(c6[2], c6[3], cx, cy, W, H);
           clip_mv(c6[4], c6[5], cx, cy, W, H);
+          bool moved = false;
 #pragma unroll
-          for (int i = 0; i < 6; i++) st.cur[i] = c6[i];
+          for (int i = 0; i < 6; i++) {
+            moved |= c6[i] != st.cur[i];
+            st.cur[i] = c6[i];
+          }
+          st.live = moved;
         }
       }
       phase_sync(coop);
+      // leave once every CU of this wave (autonomous) / item (cooperative) is settled
+      bool anyLive = false;
+      for (int k = cuB; k < cuE; k++) anyLive |= s_st[k].live != 0;
+      if (!anyLive) break;  // uniform: same flags read by every lane after the sync
+    }
+    // =============== results (affine.cl:928-957) ===============
+    if (lane < nCuW) {
+      const int k = cuB + lane;
+      const CuState& st = s_st[k];
+      const CuSlot cs = s_cu[k];
+      const int mode = cs.align * 2 + (ncp - 2);
+      const size_t idx = (size_t)ctu * (cs.align ? kHalfCusPerCtu : kFullCusPerCtu) + cs.outOff;
+      p.cost[refIdx][mode][idx] = st.bestCost;
+      vame_cpmvs_dev o;
+      o.ncps = ncp;
+      o.ltx = st.best[0]; o.lty = st.best[1]; o.rtx = st.best[2];
+      o.rty = st.best[3]; o.lbx = st.best[4]; o.lby = st.best[5];
+      p.cpmv[refIdx][mode][idx] = o;
     }
     phase_sync(coop);
   }
