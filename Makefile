@@ -26,6 +26,11 @@ ABLATE_SET ?= 1 2 4 6 7 8 11 13 14 15 16 32
 ablate:
 	@mkdir -p $(LIBDIR)
 	for a in $(ABLATE_SET); do $(HIPCC) $(HIPFLAGS) -DVAME_ABLATE=$$a -shared -o $(LIBDIR)/libvame_ablate$$a.so $(LIB_SRCS) || exit 1; done
+# profiling-only build with per-phase shader-clock counters: make phase
+phase:
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DVAME_PHASE_TIMING=1 -shared -o $(LIBDIR)/libvame_phase.so $(LIB_SRCS)
+
 cli: $(BINDIR)/vame
 
 $(LIBDIR)/libvame.so: $(LIB_SRCS) $(LIB_HDRS)
@@ -48,4 +53,4 @@ clean:
 	rm -rf $(LIBDIR) $(BINDIR)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all lib cli oracle clean resource-usage
+.PHONY: all lib cli oracle clean resource-usage ablate phase

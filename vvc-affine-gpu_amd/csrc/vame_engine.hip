@@ -447,6 +447,20 @@ const char* vame_strerror(int code) {
 }
 
 const char* vame_last_hip_error(void) { return g_hip_err; }
+
+#if VAME_PHASE_TIMING
+// profiling-only builds: per-phase shader-clock sums [kernel][phase] (see vame_kernel.h)
+int vame_debug_phase_cycles(unsigned long long* out16, int reset) {
+  if (!out16) return VAME_E_INVALID;
+  VAME_HIP(hipDeviceSynchronize());
+  VAME_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 16));
+  if (reset) {
+    unsigned long long z[16] = {};
+    VAME_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)));
+  }
+  return VAME_OK;
+}
+#endif
 const char* vame_version(void) { return "vame 0.1 (gfx950)"; }
 
 }  // extern "C"

@@ -99,6 +99,23 @@ struct KParams {
 #define VAME_ABLATE 0
 #endif
 
+// VAME_PHASE_TIMING (profiling-only builds, libvame_phase.so): every wave sums
+// the shader clock spent per phase and adds it to g_phase_cycles at exit.
+#ifndef VAME_PHASE_TIMING
+#define VAME_PHASE_TIMING 0
+#endif
+enum { kPhStage, kPhPredict, kPhCost, kPhGradient, kPhSolve, kPhTail, kNumPhases };
+#if VAME_PHASE_TIMING
+__device__ unsigned long long g_phase_cycles[2][8];  // [kernel: quad, ctu][phase]
+#define PH_DECL unsigned long long ph_acc[kNumPhases] = {}; unsigned long long ph_t = __builtin_amdgcn_s_memtime();
+#define PH_MARK(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_acc[i] += t_ - ph_t; ph_t = t_; }
+#define PH_FLUSH { if (lane == 0) for (int i_ = 0; i_ < kNumPhases; i_++) atomicAdd(&g_phase_cycles[REGION == 128][i_], ph_acc[i_]); }
+#else
+#define PH_DECL
+#define PH_MARK(i)
+#define PH_FLUSH
+#endif
+
 // ------------------------------------------------------------------ helpers
 typedef short short2v __attribute__((ext_vector_type(2)));
 
@@ -749,6 +766,7 @@ template <int REGION>
 __device__ __forceinline__ void affine_me_body(const KParams& p) {
   using C = Cfg<REGION>;
   __shared__ __attribute__((aligned(16))) uint16_t s_tile[C::TILE_ELEMS];
+  static_assert((C::TP * 2) % 16 == 0 && C::TILE % 8 == 0, "16-byte tile rows");
   __shared__ uint4 s_top[C::NSB];  // extended row 0 of every sub-block's prediction
   __shared__ uint4 s_bot[C::NSB];  // extended row 3
   __shared__ __attribute__((aligned(16))) long long s_val[kMaxCu][kNumMom];
@@ -761,6 +779,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
+  PH_DECL
 
   // ---- XCD-aware block -> (ref, ctu, item): blocks b, b+8, ... share an XCD;
   // give each XCD a contiguous run of logical work (same CTUs -> L2 reuse).
@@ -792,27 +811,43 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   const bool coop = ((hdr >> 8) & 0xFF) != 0;
   const int tx0 = ctuX + s_hdr[2] - kMargin, ty0 = ctuY + s_hdr[3] - kMargin;  // tile origin
 
-  // ---- stage the reference region (+margin) into LDS, clamp-to-edge padded
+  // ---- stage the reference region (+margin) into LDS, clamp-to-edge padded:
+  // 16-byte chunks, every load of a thread issued before its first LDS store
   {
-    constexpr int CPR = C::TILE / 4;  // 8-byte chunks per row
-    for (int ch = tid; ch < C::TILE * CPR; ch += C::THREADS) {
-      const int ty = ch / CPR, cx = (ch % CPR) * 4;
-      const int fy = clampi(ty0 + ty, 0, H - 1), fx = tx0 + cx;
-      const uint16_t* row = ref + (size_t)fy * W;
-      uint2 v;
-      if (fx >= 0 && fx + 3 < W) {
-        v = *reinterpret_cast<const uint2*>(row + fx);
-      } else {
-        unsigned a0 = row[clampi(fx, 0, W - 1)], a1 = row[clampi(fx + 1, 0, W - 1)];
-        unsigned a2 = row[clampi(fx + 2, 0, W - 1)], a3 = row[clampi(fx + 3, 0, W - 1)];
-        v.x = a0 | (a1 << 16);
-        v.y = a2 | (a3 << 16);
+    constexpr int CPR = C::TILE / 8;  // chunks per tile row
+    constexpr int NCH = C::TILE * CPR;
+    constexpr int PER = (NCH + C::THREADS - 1) / C::THREADS;
+    uint4 v[PER];
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+      const int ch = tid + j * C::THREADS;
+      if (ch < NCH) {
+        const int ty = ch / CPR, cx = (ch % CPR) * 8;
+        const int fy = clampi(ty0 + ty, 0, H - 1), fx = tx0 + cx;
+        const uint16_t* row = ref + (size_t)fy * W;
+        if (fx >= 0 && fx + 7 < W) {
+          v[j] = *reinterpret_cast<const uint4*>(row + fx);
+        } else {
+          unsigned a[8];
+#pragma unroll
+          for (int m = 0; m < 8; m++) a[m] = row[clampi(fx + m, 0, W - 1)];
+          v[j] = make_uint4(a[0] | (a[1] << 16), a[2] | (a[3] << 16), a[4] | (a[5] << 16),
+                            a[6] | (a[7] << 16));
+        }
       }
-      *reinterpret_cast<uint2*>(&s_tile[ty * C::TP + cx]) = v;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+      const int ch = tid + j * C::THREADS;
+      if (ch < NCH) *reinterpret_cast<uint4*>(&s_tile[(ch / CPR) * C::TP + (ch % CPR) * 8]) = v[j];
     }
   }
   __syncthreads();
-  if (!coop && wv >= nWaves) return;  // wave-uniform: an autonomous wave without CUs
+  PH_MARK(kPhStage)
+  if (!coop && wv >= nWaves) {  // wave-uniform: an autonomous wave without CUs
+    PH_FLUSH
+    return;
+  }
 
   // ---- CUs of this wave, this lane's CU and sub-blocks (fixed for the item)
   int cuB, cuE, logL, lidx;
@@ -940,6 +975,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         }
       }
       phase_sync(coop);
+      PH_MARK(kPhPredict)
 
       // =============== cost, best update (affine.cl:416-457) ===============
       const bool lastIter = iter == niter;
@@ -957,6 +993,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         }
         st.satd = 0;
       }
+      PH_MARK(kPhCost)
       if (lastIter) break;  // uniform
 
       // =============== gradients + normal equations (affine.cl:477-752) ===============
@@ -979,6 +1016,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         }
       }
       phase_sync(coop);
+      PH_MARK(kPhGradient)
 
       // =============== solve + CPMV update (affine.cl:782-893), per CU segment ===============
       if (!(VAME_ABLATE & 1)) {
@@ -1023,6 +1061,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         }
       }
       phase_sync(coop);
+      PH_MARK(kPhSolve)
       // leave once every CU of this wave (autonomous) / item (cooperative) is settled
       bool anyLive = false;
       for (int k = cuB; k < cuE; k++) anyLive |= s_st[k].live != 0;
@@ -1043,7 +1082,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       p.cpmv[refIdx][mode][idx] = o;
     }
     phase_sync(coop);
+    PH_MARK(kPhTail)
   }
+  PH_FLUSH
 }
 
 // Distinct entry points so profiles tell the two work-item classes apart.
