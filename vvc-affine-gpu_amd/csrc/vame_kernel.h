@@ -377,7 +377,9 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   for (int r = 0; r < 4; r++)
     O[r] = *reinterpret_cast<const uint2*>(cur + (size_t)(g.y + sy + r) * W + g.x + sx);
   const int px = f.spread ? (g.w >> 1) : sx + 2, py = f.spread ? (g.h >> 1) : sy + 2;
-  int mx = f.bx + f.hx * px + f.vx * py, my = f.by + f.hy * px + f.vy * py;
+  // |h|, |v| < 2^22 (clamped CPMVs, << (7 - log2 size)), px, py <= 128: 24-bit products are exact
+  int mx = f.bx + __mul24(f.hx, px) + __mul24(f.vx, py);
+  int my = f.by + __mul24(f.hy, px) + __mul24(f.vy, py);
   mx = (mx + 64 - (mx >= 0)) >> 7;  // roundMv (aux_functions.cl:38-47)
   my = (my + 64 - (my >= 0)) >> 7;
   clip_mv(mx, my, g.x, g.y, W, H);
@@ -682,33 +684,35 @@ struct Cfg {
 //        symmetric matrix, then b0..b3 (before the << 3);
 //   3 CP (affine.cl:684-689): the moments {1,u,v,uu,uv,vv} x {xx,xy,yy}, then
 //        {1,u,v} x {xe,ye}; solve_cu forms the matrix from them.
+__device__ __forceinline__ long long mul64(int a, int b) { return (long long)a * (long long)b; }
+
 template <int NCP>
 __device__ __forceinline__ long long eq_value(int i, const int (&S)[5], int u, int v) {
-  const long long xx = S[0], xy = S[1], yy = S[2], xe = S[3], ye = S[4];
-  const long long U = u, V = v;
+  // monomials fit int32 (u, v <= 126); every product is one i32 x i32 -> i64
+  const int xx = S[0], xy = S[1], yy = S[2], xe = S[3], ye = S[4];
+  const int uu = u * u, uv = u * v, vv = v * v;
   if constexpr (NCP == 2) {
     switch (i) {
       case 0: return xx;
-      case 1: return U * xx + V * xy;
+      case 1: return mul64(u, xx) + mul64(v, xy);
       case 2: return xy;
-      case 3: return V * xx - U * xy;
-      case 4: return (U * U) * xx + (2 * U * V) * xy + (V * V) * yy;
-      case 5: return U * xy + V * yy;
-      case 6: return (U * V) * xx + (V * V - U * U) * xy - (U * V) * yy;
+      case 3: return mul64(v, xx) - mul64(u, xy);
+      case 4: return mul64(uu, xx) + mul64(2 * uv, xy) + mul64(vv, yy);
+      case 5: return mul64(u, xy) + mul64(v, yy);
+      case 6: return mul64(uv, xx) + mul64(vv - uu, xy) - mul64(uv, yy);
       case 7: return yy;
-      case 8: return V * xy - U * yy;
-      case 9: return (V * V) * xx - (2 * U * V) * xy + (U * U) * yy;
+      case 8: return mul64(v, xy) - mul64(u, yy);
+      case 9: return mul64(vv, xx) - mul64(2 * uv, xy) + mul64(uu, yy);
       case 10: return xe;
-      case 11: return U * xe + V * ye;
+      case 11: return mul64(u, xe) + mul64(v, ye);
       case 12: return ye;
-      default: return V * xe - U * ye;
+      default: return mul64(v, xe) - mul64(u, ye);
     }
   } else {
     const int sidx = i < 18 ? i / 6 : (i < 21 ? 3 : 4);
     const int mono = i < 18 ? i % 6 : (i - 18) % 3;
-    const long long m = mono == 0 ? 1 : mono == 1 ? U : mono == 2 ? V : mono == 3 ? U * U
-                        : mono == 4 ? U * V : V * V;
-    return m * (long long)S[sidx];
+    const int m = mono == 0 ? 1 : mono == 1 ? u : mono == 2 ? v : mono == 3 ? uu : mono == 4 ? uv : vv;
+    return mul64(m, S[sidx]);
   }
 }
 
@@ -734,9 +738,9 @@ __device__ __forceinline__ int seg_sum_c(int v) {
 // segment's sums into the CU's LDS row.  Each int64 value x is reduced as two
 // int32 halves, x = hi * 2^24 + lo with lo in [0, 2^24): |x| < 2^44, so over
 // at most 64 lanes sum(lo) < 2^30 and |sum(hi)| < 2^26 -- exact.
-template <int NCP, int LOGS>
+template <int NCP, int LOGS, bool COOP>
 __device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int v, bool leader,
-                                                   bool coop, long long* dst) {
+                                                   long long* dst) {
   constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
 #pragma unroll
   for (int i = 0; i < NV; i++) {
@@ -745,7 +749,7 @@ __device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int
     const int hi = seg_sum_c<LOGS>((int)(x >> 24));
     if (leader) {
       const long long r = (long long)hi * (1ll << 24) + (long long)(unsigned)lo;
-      if (coop)
+      if (COOP)
         atomicAdd(reinterpret_cast<unsigned long long*>(&dst[i]), (unsigned long long)r);
       else
         dst[i] = r;
@@ -755,10 +759,14 @@ __device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int
 template <int NCP>
 __device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v, int logS,
                                                  bool leader, bool coop, long long* dst) {
-  switch (logS) {  // wave-uniform; work items only hold CUs of 16, 32 or >= 64 sub-blocks
-    case 4: reduce_equations_c<NCP, 4>(S, u, v, leader, coop, dst); break;
-    case 5: reduce_equations_c<NCP, 5>(S, u, v, leader, coop, dst); break;
-    default: reduce_equations_c<NCP, 6>(S, u, v, leader, coop, dst); break;
+  if (coop) {  // cooperative items: whole-wave segments, partial sums meet in LDS atomics
+    reduce_equations_c<NCP, 6, true>(S, u, v, leader, dst);
+    return;
+  }
+  switch (logS) {  // wave-uniform; autonomous waves hold CUs of 16, 32 or 64 sub-blocks
+    case 4: reduce_equations_c<NCP, 4, false>(S, u, v, leader, dst); break;
+    case 5: reduce_equations_c<NCP, 5, false>(S, u, v, leader, dst); break;
+    default: reduce_equations_c<NCP, 6, false>(S, u, v, leader, dst); break;
   }
 }
 
