@@ -14,10 +14,10 @@ BINDIR  := $(PKG)/bin
 # (explicit fma where OpenCL's FP_CONTRACT fuses); integer paths are unaffected.
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
 
-LIB_SRCS := $(CSRC)/vame_engine.hip $(CSRC)/vame_hostlogic.cpp
+LIB_SRCS := $(CSRC)/vame_engine.hip $(CSRC)/vame_hostlogic.cpp $(CSRC)/vame_io.cpp
 LIB_HDRS := $(CSRC)/vame_kernel.h $(CSRC)/vame_tables.h include/vame.h
 
-all: lib oracle
+all: lib cli oracle
 
 lib: $(LIBDIR)/libvame.so
 
@@ -37,9 +37,9 @@ $(LIBDIR)/libvame.so: $(LIB_SRCS) $(LIB_HDRS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(LIB_SRCS)
 
-$(BINDIR)/vame: $(PKG)/host/vame_main.cpp $(PKG)/host/vame_io.cpp $(PKG)/host/vame_io.h $(LIBDIR)/libvame.so
+$(BINDIR)/vame: $(PKG)/host/vame_main.cpp include/vame.h $(LIBDIR)/libvame.so
 	@mkdir -p $(BINDIR)
-	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $(PKG)/host/vame_main.cpp $(PKG)/host/vame_io.cpp \
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $(PKG)/host/vame_main.cpp \
 	    -L$(LIBDIR) -lvame -Wl,-rpath,'$$ORIGIN/../lib' -lpthread
 
 oracle:

@@ -101,6 +101,33 @@ int vame_poc_qp(int qp, int poc);
  * with the POC held by each refIdx slot; returns the number of refs. */
 int vame_ref_list(int poc, int* pocs);
 
+/* ---- Host I/O contracts of the reference's ./main (no device work) ---- */
+
+/* Frame ingest (main.cpp:293-330): reads `nframes` frames of width x height
+ * samples into `out` (host, nframes*W*H uint16).  CSV layout as the reference
+ * reads it: one frame line per text line, ',' separated, frames stacked; each
+ * value parsed like stoi and stored as unsigned short.  Paths ending in .u16 /
+ * .yuv are raw little-endian 16-bit frames.  nthreads <= 0: all host cores.
+ * Returns 0, or VAME_E_INVALID for a missing file / short file / bad value. */
+int vame_read_frames(const char* path, int width, int height, int nframes, uint16_t* out,
+                     int nthreads);
+
+/* Decision log (main_aux_functions.h:387-525, 1547-1585).  pred = 0 FULL_2CP,
+ * 1 FULL_3CP, 2 HALF_2CP, 3 HALF_3CP (constants.h:15-21).  Files are
+ * <prefix>_<FULL|HALF>_<2|3>CPs_<W>x<H>.csv with the reference's header.
+ *   vame_log_remove_old    : removeOldTraces (:1547) -- deletes the old files
+ *   vame_log_write_headers : creates/truncates the files of one pred with the
+ *                            header (done by the reference at POC 1, refIdx 0)
+ *   vame_log_append        : appends the rows of one (POC, refIdx, pred) from
+ *                            HOST result arrays in the reference's index layout;
+ *                            returns the number of bytes written (< 0: error)
+ *   vame_log_file_count    : distinct files of a pred (12 FULL, 8 HALF)        */
+int vame_log_remove_old(const char* prefix);
+int vame_log_write_headers(const char* prefix, int pred);
+long long vame_log_append(const char* prefix, int pred, int width, int height, int poc, int ref,
+                          const int64_t* cost, const vame_cpmvs* cpmvs, int nthreads);
+int vame_log_file_count(int pred);
+
 const char* vame_strerror(int code);
 const char* vame_last_hip_error(void);
 const char* vame_version(void);

@@ -7,6 +7,11 @@ reference checkout exists; the output JSON is what the tests read).
   table parsed as data from constants.h:94.
 * reference list per POC: the reference's own debug replay of the ring
   (testReferences, main_aux_functions.h:1499-1545), restated.
+* decision-log tables: the host-side arrays the log writer indexes
+  (reportAffineResultsMaster_new, main_aux_functions.h:387-525) parsed as data
+  from constants.h -- WIDTH/HEIGHT_LIST, RETURN_STRIDE_LIST, HA_WIDTH/HEIGHT_LIST,
+  HA_RETURN_STRIDE_LIST, HA_ALL_X_POS / HA_ALL_Y_POS -- with the per-group CU
+  count rule of main_aux_functions.h:447-450.
 """
 import json
 import math
@@ -59,6 +64,48 @@ def ref_lists(n):
     return out
 
 
+def _c_array(src, name):
+    """Integer initialiser of `name[...] = {...}` in constants.h (1-D or 2-D)."""
+    i = re.search(r"\b" + name + r"\[", src).start()
+    i = src.index("=", i)
+    j = src.index("{", i)
+    depth, k = 0, j
+    while True:
+        if src[k] == "{":
+            depth += 1
+        elif src[k] == "}":
+            depth -= 1
+            if depth == 0:
+                break
+        k += 1
+    body = re.sub(r"/\*.*?\*/|//[^\n]*", "", src[j:k + 1], flags=re.S)
+    if body.count("{") > 1:
+        rows = re.findall(r"\{([^{}]*)\}", body)
+        return [[int(eval(v.strip())) for v in r.split(",") if v.strip()] for r in rows]
+    return [int(eval(v.strip())) for v in body.strip().strip("{}").split(",") if v.strip()]
+
+
+def log_tables():
+    src = open(os.path.join(REF, "constants.h")).read()
+    t = {n: _c_array(src, n) for n in ("WIDTH_LIST", "HEIGHT_LIST", "RETURN_STRIDE_LIST",
+                                       "HA_WIDTH_LIST", "HA_HEIGHT_LIST", "HA_RETURN_STRIDE_LIST",
+                                       "HA_ALL_X_POS", "HA_ALL_Y_POS")}
+    # main_aux_functions.h:447-450: the last group of each list has a fixed count
+    full_n = [64 if g == 11 else t["RETURN_STRIDE_LIST"][g + 1] - t["RETURN_STRIDE_LIST"][g]
+              for g in range(12)]
+    half_n = [32 if g == 23 else t["HA_RETURN_STRIDE_LIST"][g + 1] - t["HA_RETURN_STRIDE_LIST"][g]
+              for g in range(24)]
+    full = [{"w": t["WIDTH_LIST"][g], "h": t["HEIGHT_LIST"][g], "n": full_n[g],
+             "stride": t["RETURN_STRIDE_LIST"][g]} for g in range(12)]
+    half = [{"w": t["HA_WIDTH_LIST"][g], "h": t["HA_HEIGHT_LIST"][g], "n": half_n[g],
+             "stride": t["HA_RETURN_STRIDE_LIST"][g],
+             "x": t["HA_ALL_X_POS"][g][:half_n[g]], "y": t["HA_ALL_Y_POS"][g][:half_n[g]]}
+            for g in range(24)]
+    for g in half:
+        assert len(g["x"]) == g["n"] and len(g["y"]) == g["n"], g
+    return {"full": full, "half": half}
+
+
 def main():
     lam = full_lambdas()
     rows = []
@@ -67,7 +114,8 @@ def main():
             q = compute_delta_qp(qp, poc)
             rows.append({"qp": qp, "poc": poc, "poc_qp": q, "lambda": lam[q]})
     refs = ref_lists(64)
-    out = {"lambda": rows, "ref_lists": {str(k): v for k, v in refs.items()}}
+    out = {"lambda": rows, "ref_lists": {str(k): v for k, v in refs.items()},
+           "log_tables": log_tables()}
     json.dump(out, open(os.path.join(HERE, "hostlogic.json"), "w"), indent=0)
     print(f"{len(rows)} lambda rows, {len(refs)} ref lists")
 

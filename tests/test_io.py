@@ -1,0 +1,228 @@
+"""CPU tests of the host I/O contracts (csrc/vame_io.cpp through libvame.so):
+frame ingest vs the reference's reader semantics, and the decision-log writer
+byte-for-byte vs the restatement of reportAffineResultsMaster_new
+(tests/oracle_log.py), fed with the reference kernels' own outputs
+(tests/golden/*.npz).  Also the CLI's argument handling (no GPU needed)."""
+import glob
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from vame import logs
+from vame.synth import synth_sequence, write_csv
+
+import oracle_log as OL
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = sorted(glob.glob(os.path.join(REPO, "tests", "golden", "*.npz")))
+CLI = os.path.join(REPO, "vvc-affine-gpu_amd", "bin", "vame")
+MODES = ("FULL_2CP", "FULL_3CP", "HALF_2CP", "HALF_3CP")
+
+
+# ------------------------------------------------------------------ ingest
+@pytest.fixture(scope="module")
+def seq416():
+    return synth_sequence(416, 240, 3, qp=32)
+
+
+@pytest.mark.parametrize("nthreads", [1, 3, 8])
+def test_read_csv_matches_writer(tmp_path, seq416, nthreads):
+    orig, recon = seq416
+    p = str(tmp_path / "orig.csv")
+    write_csv(p, orig)
+    got = logs.read_frames(p, 416, 240, 3, nthreads)
+    assert got.dtype == np.uint16 and (got == orig).all()
+    # fewer frames than the file holds: only the first ones are read
+    assert (logs.read_frames(p, 416, 240, 2, nthreads) == orig[:2]).all()
+
+
+def test_read_csv_reference_semantics(tmp_path):
+    """getline(',') + stoi per value: leading blanks, trailing commas, CRLF,
+    '+' signs, text after the digits, extra columns, no final newline."""
+    rng = np.random.default_rng(7)
+    fr = rng.integers(0, 1024, size=(2, 240, 416)).astype(np.uint16)
+    lines = []
+    for k in range(2):
+        for h in range(240):
+            v = [str(x) for x in fr[k, h]]
+            if h % 5 == 1:
+                v = [" " + s for s in v]
+            if h % 7 == 2:
+                v[0] = v[0].replace(v[0].strip(), "+" + v[0].strip())
+            if h % 11 == 3:
+                v[3] = v[3] + "abc"
+            line = ",".join(v)
+            if h % 3 == 0:
+                line += ","
+            if h % 4 == 0:
+                line += ",99,98"  # extra columns are ignored
+            if h % 6 == 5:
+                line += "\r"
+            lines.append(line)
+    p = tmp_path / "odd.csv"
+    p.write_text("\n".join(lines))  # no trailing newline
+    got = logs.read_frames(str(p), 416, 240, 2, 4)
+    assert (got == fr).all()
+    assert (OL.read_frames(str(p), 416, 240, 2) == fr).all()
+
+
+def test_read_frames_errors_and_raw(tmp_path):
+    rng = np.random.default_rng(3)
+    fr = rng.integers(0, 1024, size=(1, 240, 416)).astype(np.uint16)
+    p = str(tmp_path / "one.csv")
+    write_csv(p, fr)
+    with pytest.raises(Exception):
+        logs.read_frames(p, 416, 240, 2)  # short file
+    with pytest.raises(Exception):
+        logs.read_frames(str(tmp_path / "missing.csv"), 416, 240, 1)
+    bad = tmp_path / "bad.csv"
+    bad.write_text("1,2,x3\n" * 240)
+    with pytest.raises(Exception):
+        logs.read_frames(str(bad), 3, 240, 1)
+    short = tmp_path / "short.csv"
+    short.write_text("1,2\n" * 240)
+    with pytest.raises(Exception):
+        logs.read_frames(str(short), 3, 240, 1)
+    raw = str(tmp_path / "f.u16")
+    fr.tofile(raw)
+    assert (logs.read_frames(raw, 416, 240, 1) == fr).all()
+
+
+def test_read_csv_large_multithreaded(tmp_path):
+    """Many byte ranges, lines straddling range cuts: 832x480, 2 frames, 16 threads."""
+    rng = np.random.default_rng(11)
+    fr = rng.integers(0, 1024, size=(2, 480, 832)).astype(np.uint16)
+    p = str(tmp_path / "big.csv")
+    write_csv(p, fr)
+    for t in (2, 7, 16, 64):
+        assert (logs.read_frames(p, 832, 480, 2, t) == fr).all()
+
+
+# ------------------------------------------------------------------ decision log
+def _files(d):
+    return sorted(os.listdir(d))
+
+
+def _golden_results(z):
+    return {m: (z[m + "_cost"], np.concatenate([np.full((len(z[m + "_cost"]), 1), 2 + (i & 1),
+                                                        np.int32), z[m + "_cpmv"]], 1))
+            for i, m in enumerate(MODES)}
+
+
+@pytest.mark.parametrize("path", GOLDEN[:4], ids=[os.path.basename(p)[:-4] for p in GOLDEN[:4]])
+def test_log_writer_byte_identical(tmp_path, path):
+    z = np.load(path)
+    W, H = int(z["W"]), int(z["H"])
+    res = _golden_results(z)
+    a, b = tmp_path / "native", tmp_path / "restated"
+    a.mkdir()
+    b.mkdir()
+    # two (POC, ref) appends after the headers, like POC 1 ref 0 then POC 2 ref 1
+    for pred, m in enumerate(MODES):
+        cost, cp = res[m]
+        logs.write_headers(str(a / "log"), pred)
+        OL.write_headers(str(b / "log"), pred)
+        for poc, ref in ((1, 0), (2, 1)):
+            nb = logs.append(str(a / "log"), pred, W, H, poc, ref, cost, cp, nthreads=3)
+            assert nb > 0
+            OL.append(str(b / "log"), pred, W, H, poc, ref, cost, cp)
+    fa, fb = _files(a), _files(b)
+    assert fa == fb
+    assert len(fa) == 40  # 12 FULL + 8 HALF names, x {2, 3} CPs
+    for f in fa:
+        assert (a / f).read_bytes() == (b / f).read_bytes(), f
+    # row count: every candidate CU of every CTU, twice
+    n_ctus = logs.lib().vame_num_ctus(W, H)
+    for pred in range(4):
+        rows = sum(len((a / f).read_text().splitlines()) - 1
+                   for f in fa if OL.TYPES[pred] in "_" + f[4:])
+        assert rows == 2 * n_ctus * (284 if pred >= 2 else 201)
+
+
+def test_log_counts_and_remove_old(tmp_path):
+    assert [logs.lib().vame_log_file_count(p) for p in range(4)] == [12, 12, 8, 8]
+    pre = str(tmp_path / "x")
+    for pred in range(4):
+        logs.write_headers(pre, pred)
+    assert len(_files(tmp_path)) == 40
+    (tmp_path / "keep.csv").write_text("k")
+    logs.remove_old(pre)
+    assert _files(tmp_path) == ["keep.csv"]
+    # the restated removeOldTraces covers the same names
+    for pred in range(4):
+        OL.write_headers(pre, pred)
+    OL.remove_old(pre)
+    assert _files(tmp_path) == ["keep.csv"]
+
+
+def test_write_poc_order(tmp_path):
+    """write_poc == the reference's per-POC sequence (refIdx outer, PRED inner)."""
+    z = np.load(GOLDEN[0])
+    W, H = int(z["W"]), int(z["H"])
+    res = _golden_results(z)
+    results = {(r, m): res[m] for r in range(2) for m in MODES}
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    for poc in (1, 2):
+        logs.write_poc(str(a / "p"), W, H, poc, results, nthreads=2)
+        for r in range(2):
+            for pred, m in enumerate(MODES):
+                if poc == 1 and r == 0:
+                    OL.write_headers(str(b / "p"), pred)
+                OL.append(str(b / "p"), pred, W, H, poc, r, *res[m])
+    for f in _files(a):
+        assert (a / f).read_bytes() == (b / f).read_bytes(), f
+
+
+def test_log_tables_equal_kernel_geometry():
+    """The host tables the reference's writer indexes (constants.h) are the
+    kernel's CU geometry (constants.cl) restated in vame_tables.h."""
+    from vame.hostlogic import geometry
+    for align, key in ((0, "full"), (1, "half")):
+        geo = geometry(align)
+        for g, t in enumerate(OL.TABLES[key]):
+            w, h, xs, ys, stride = geo[g]
+            assert (w, h, len(xs), stride) == (t["w"], t["h"], t["n"], t["stride"]), (key, g)
+            if align:
+                assert list(xs) == t["x"] and list(ys) == t["y"], g
+            else:
+                k = np.arange(t["n"])
+                assert list(xs) == list((k * w) % 128) and list(ys) == list((k * w) // 128 * h)
+
+
+# ------------------------------------------------------------------ CLI (no GPU)
+def _run(args, cwd):
+    return subprocess.run([CLI] + args, cwd=cwd, capture_output=True, text=True, timeout=60)
+
+
+def test_cli_help_and_parameter_errors(tmp_path):
+    r = _run(["--help"], tmp_path)
+    assert r.returncode == 1 and "--FramesToBeEncoded" in r.stdout and "-q [ --QP ]" in r.stdout
+    r = _run(["-q", "32"], tmp_path)
+    assert r.returncode == 1
+    for msg in ("QP=32", "[!] ERROR: FramesToBeEncoded not set.", "[!] ERROR: Resolution not set.",
+                "[!] ERROR: Input original frames not set.",
+                "Exiting after finding errors in input parameters"):
+        assert msg in r.stdout, msg
+    r = _run(["--bogus", "1"], tmp_path)
+    assert r.returncode == 1 and "unrecognised option" in r.stderr
+    # boost-style forms: -q32, --QP=32, unique long prefix (--Frames), defaults reported
+    r = _run(["-q32", "--Frames=3", "--Res", "416x240", "-o", "a", "-r", "b",
+              "--ExtraGradientIter", "2"], tmp_path)
+    for msg in ("QP=32", "FramesToBeEncoded=3", "Resolution=416x240", "InputOriginalFrame=a",
+                "ExtraGradientIter=2. Using a total of 7 iterations for 2 CPs and 6 iterations",
+                "Device index not set. Using standard value of 0.",
+                "CPMVs log file not set."):
+        assert msg in r.stdout, msg
+
+
+def test_cli_no_device_or_bad_resolution(tmp_path):
+    """Without a HIP device the CLI stops like the reference with a bad index."""
+    r = _run(["-q", "32", "-f", "1", "-s", "416x240", "-o", "a", "-r", "b"], tmp_path)
+    if "Incorrect GPU index" in r.stdout:
+        assert r.returncode == 0
+    else:  # a GPU is present: then the inputs are missing
+        assert r.returncode == 1 and "error while opening samples files" in r.stderr

@@ -1,0 +1,712 @@
+// vame_main.cpp -- `vame`, the drop-in for the reference's ./main
+// (main.cpp:53-1122): same flags and defaults, same CSV inputs, same per-CU
+// decision logs (byte for byte), same stdout report keys -- with the affine ME
+// running as HIP kernels on MI355X through libvame.so (include/vame.h).
+//
+//   vame -f N -s WxH -q QP -o orig.csv -r recon.csv [-l prefix]
+//        [--ExtraGradientIter K] [--DeviceIndex D]
+//   extensions: --gpus G      frame-shard POCs over G devices (D .. D+G-1),
+//                             one host thread + context per device
+//               --devices L   explicit device list (e.g. 0,1,2,3)
+//               --modes all|2cp   all four PREDs (default) or the 2-CP ones
+//               --per-launch  one launch per (refIdx, PRED) as the reference
+//                             does (per-PRED kernel times); default = fused
+//                             per-POC launch (vame_affine_me_poc)
+//               --threads T   host threads for CSV parsing / log formatting
+//
+// Differences to the reference host, all deliberate:
+//  * the 4-slot reference ring (main.cpp:591-707) is label bookkeeping only:
+//    every recon frame is uploaded once and refIdx r points at the frame the
+//    ring holds (vame_ref_list), so the ring's D2D copies disappear;
+//  * it keeps 4 slots for any N (the reference allocates N_FRAMES ring buffers
+//    into a 4-entry array, main.cpp:343-349);
+//  * results are copied back asynchronously and the logs are formatted on the
+//    host while the GPU runs the next POC; stdout keeps the reference's order;
+//  * the OpenCL platform/device listing becomes a HIP device listing, and the
+//    per-PRED START/FINISH EXEC timestamps are not printed (PREDs are fused).
+#include <hip/hip_runtime.h>
+#include <sys/time.h>
+#include <time.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/vame.h"
+
+namespace {
+
+// ------------------------------------------------------------ options
+struct Opt {
+  const char* name;
+  char shortc;
+  bool has_default;
+  std::string def;
+  const char* help;
+  bool set = false;
+  std::string val;
+};
+
+struct Cli {
+  std::vector<Opt> opts;
+  std::vector<std::string> flags_set;  // value-less extension flags
+  int find(const std::string& n) {
+    for (size_t i = 0; i < opts.size(); i++)
+      if (n == opts[i].name) return (int)i;
+    // boost's allow_guessing: a unique prefix of a long option name
+    int hit = -1;
+    for (size_t i = 0; i < opts.size(); i++)
+      if (strncmp(opts[i].name, n.c_str(), n.size()) == 0) {
+        if (hit >= 0) return -2;
+        hit = (int)i;
+      }
+    return hit;
+  }
+  int find_short(char c) {
+    for (size_t i = 0; i < opts.size(); i++)
+      if (opts[i].shortc == c) return (int)i;
+    return -1;
+  }
+  bool has(const char* n) { return opts[find(n)].set; }
+  std::string str(const char* n) {
+    Opt& o = opts[find(n)];
+    return o.set ? o.val : o.def;
+  }
+  int num(const char* n) { return atoi(str(n).c_str()); }
+  bool defaulted(const char* n) { return !opts[find(n)].set; }
+};
+
+void print_help(Cli& c) {
+  printf("Allowed options:\n");
+  printf("  -h [ --help ]                         produce help message\n");
+  for (auto& o : c.opts) {
+    char lhs[96];
+    if (o.shortc)
+      snprintf(lhs, sizeof lhs, "  -%c [ --%s ] arg%s", o.shortc, o.name,
+               o.has_default ? (" (=" + o.def + ")").c_str() : "");
+    else
+      snprintf(lhs, sizeof lhs, "  --%s arg%s", o.name,
+               o.has_default ? (" (=" + o.def + ")").c_str() : "");
+    printf("%-40s%s\n", lhs, o.help);
+  }
+  printf("%-40s%s\n", "  --per-launch",
+         "one launch per (refIdx, PRED) like the reference (per-PRED kernel times)");
+}
+
+// Returns 0 ok, 1 help, 2 error.
+int parse(Cli& c, int argc, char** argv) {
+  for (int i = 1; i < argc; i++) {
+    std::string a = argv[i];
+    int idx = -1;
+    std::string val;
+    bool have_val = false;
+    if (a.size() > 2 && a[0] == '-' && a[1] == '-') {
+      std::string n = a.substr(2);
+      size_t eq = n.find('=');
+      if (eq != std::string::npos) {
+        val = n.substr(eq + 1);
+        n = n.substr(0, eq);
+        have_val = true;
+      }
+      if (n == "help") return 1;
+      if (n == "per-launch") {
+        c.flags_set.push_back(n);
+        continue;
+      }
+      idx = c.find(n);
+      if (idx == -2) {
+        fprintf(stderr, "option '--%s' is ambiguous\n", n.c_str());
+        return 2;
+      }
+    } else if (a.size() >= 2 && a[0] == '-') {
+      if (a[1] == 'h' && a.size() == 2) return 1;
+      idx = c.find_short(a[1]);
+      if (a.size() > 2) {
+        val = a.substr(2);
+        have_val = true;
+      }
+    } else {
+      fprintf(stderr, "unexpected positional argument '%s'\n", a.c_str());
+      return 2;
+    }
+    if (idx < 0) {
+      fprintf(stderr, "unrecognised option '%s'\n", a.c_str());
+      return 2;
+    }
+    if (!have_val) {
+      if (i + 1 >= argc) {
+        fprintf(stderr, "the required argument for option '--%s' is missing\n", c.opts[idx].name);
+        return 2;
+      }
+      val = argv[++i];
+    }
+    c.opts[idx].set = true;
+    c.opts[idx].val = val;
+  }
+  return 0;
+}
+
+// main_aux_functions.h:77-145 checkReportParameters
+int check_report(Cli& c) {
+  int errors = 0;
+  printf("-=-= INPUT PARAMETERS =-=-\n");
+  if (c.defaulted("DeviceIndex"))
+    printf("  Device index not set. Using standard value of %d.\n", c.num("DeviceIndex"));
+  else
+    printf("  Device Index=%d\n", c.num("DeviceIndex"));
+  if (c.defaulted("CpmvLogFile"))
+    printf("  CPMVs log file not set. The output will not be written to any file.\n");
+  else
+    printf("  CpmvLogFile=%s\n", c.str("CpmvLogFile").c_str());
+  if (c.has("QP"))
+    printf("  QP=%d\n", c.num("QP"));
+  else {
+    printf("  [!] ERROR: QP not set.\n");
+    errors++;
+  }
+  if (c.has("FramesToBeEncoded"))
+    printf("  FramesToBeEncoded=%d\n", c.num("FramesToBeEncoded"));
+  else {
+    printf("  [!] ERROR: FramesToBeEncoded not set.\n");
+    errors++;
+  }
+  if (c.defaulted("ExtraGradientIter"))
+    printf("  ExtraGradientIter not specified. Using zero extra gradients (i.e., 5 iterations for 2 "
+           "CPs and 4 iterations for 3 CPs).\n");
+  else {
+    const int e = c.num("ExtraGradientIter");
+    printf("  ExtraGradientIter=%d. Using a total of %d iterations for 2 CPs and %d iterations for "
+           "3 CPs.\n",
+           e, 5 + e, 4 + e);
+  }
+  if (c.has("Resolution"))
+    printf("  Resolution=%s\n", c.str("Resolution").c_str());
+  else {
+    printf("  [!] ERROR: Resolution not set.\n");
+    errors++;
+  }
+  if (c.has("OriginalFrames"))
+    printf("  InputOriginalFrame=%s\n", c.str("OriginalFrames").c_str());
+  else {
+    printf("  [!] ERROR: Input original frames not set.\n");
+    errors++;
+  }
+  if (c.has("ReferenceFrames"))
+    printf("  InputReferenceFrame=%s\n", c.str("ReferenceFrames").c_str());
+  else {
+    printf("  [!] ERROR: Input reference frames not set.\n");
+    errors++;
+  }
+  return errors;
+}
+
+// main_aux_functions.h:59-68
+void print_timestamp(const char* msg) {
+  struct timeval tv;
+  gettimeofday(&tv, nullptr);
+  struct tm* t = localtime(&tv.tv_sec);
+  printf("%s @ %02d:%02d:%02d.%03d\n", msg, t->tm_hour, t->tm_min, t->tm_sec,
+         (int)(tv.tv_usec / 1000));
+}
+
+double now_s() {
+  struct timeval tv;
+  gettimeofday(&tv, nullptr);
+  return (double)tv.tv_sec + (double)tv.tv_usec / 1e6;
+}
+
+// main_aux_functions.h:1499-1545 testReferences (prints POC 1 .. N-1)
+void test_references(int n_frames, int qp) {
+  printf("-=-=-= Artificial references used for debugging =-=-=-=-\n");
+  printf("Input QP = %d\n", qp);
+  for (int f = 1; f < n_frames; f++) {
+    int refs[4];
+    const int n = vame_ref_list(f, refs);
+    printf("POC %3d   QP %d motionLambda %f : [L0 %d", f, vame_poc_qp(qp, f),
+           (double)vame_lambda(qp, f), refs[0]);
+    for (int r = 1; r < n; r++) printf(" %d", refs[r]);
+    printf("]\n");
+  }
+}
+
+// ------------------------------------------------------------ results
+constexpr int kFull = 201, kHalf = 284;
+
+struct Layout {  // one POC's results: [ref][pred] cost block, then cpmvs block
+  size_t off_cost[4][4], off_cp[4][4], bytes;
+  Layout(int nCtus) {
+    size_t o = 0;
+    for (int r = 0; r < 4; r++)
+      for (int m = 0; m < 4; m++) {
+        const size_t n = (size_t)nCtus * ((m >> 1) ? kHalf : kFull);
+        off_cost[r][m] = o;
+        o += n * sizeof(int64_t);
+        off_cp[r][m] = o;
+        o += (n * sizeof(vame_cpmvs) + 255) & ~size_t(255);
+      }
+    bytes = o;
+  }
+};
+
+struct Slab {
+  char* host = nullptr;  // pinned
+  int poc = 0, nrefs = 0;
+  float pred_ns[4] = {0, 0, 0, 0};  // per-launch mode kernel times
+  float fused_ns = 0;
+};
+
+struct Shared {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Slab*> pool;
+  std::map<int, Slab*> done;
+  std::string error;
+  bool failed = false;
+};
+
+struct Job {
+  int device, W, H, nCtus, qp, extra, mode_mask;
+  bool per_launch;
+  std::vector<int> pocs;
+  const uint16_t* orig;   // host, POC p at frame p-1
+  const uint16_t* recon;  // host, POC p at frame p
+  const Layout* L;
+  Shared* S;
+};
+
+#define GPU_CHECK(x, what)                                                               \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      fail(S, std::string(what) + ": " + hipGetErrorString(e_));                         \
+      return;                                                                            \
+    }                                                                                    \
+  } while (0)
+#define VAME_CHECK(x, what)                                                              \
+  do {                                                                                   \
+    int rc_ = (x);                                                                       \
+    if (rc_ != 0) {                                                                      \
+      fail(S, std::string(what) + ": " + vame_strerror(rc_) + " " + vame_last_hip_error()); \
+      return;                                                                            \
+    }                                                                                    \
+  } while (0)
+
+void fail(Shared* S, const std::string& msg) {
+  std::lock_guard<std::mutex> g(S->mu);
+  if (!S->failed) S->error = msg;
+  S->failed = true;
+  S->cv.notify_all();
+}
+
+// One device: uploads the frames its POCs need, runs them in order on one
+// stream, and hands each POC's results (pinned host slab) to the writer.
+void gpu_worker(Job J) {
+  Shared* S = J.S;
+  GPU_CHECK(hipSetDevice(J.device), "hipSetDevice");
+  vame_ctx* ctx = nullptr;
+  VAME_CHECK(vame_create(&ctx, J.device, J.W, J.H), "vame_create");
+  hipStream_t st;
+  GPU_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+  const size_t fsz = (size_t)J.W * J.H;
+  // frames: orig of each POC, recon of every label its ring holds
+  std::map<int, uint16_t*> dorig, drecon;
+  for (int p : J.pocs) {
+    GPU_CHECK(hipMalloc(&dorig[p], fsz * 2), "hipMalloc frame");
+    GPU_CHECK(hipMemcpyAsync(dorig[p], J.orig + (size_t)(p - 1) * fsz, fsz * 2,
+                             hipMemcpyHostToDevice, st),
+              "upload orig");
+    int refs[4];
+    const int n = vame_ref_list(p, refs);
+    for (int r = 0; r < n; r++)
+      if (!drecon.count(refs[r])) {
+        GPU_CHECK(hipMalloc(&drecon[refs[r]], fsz * 2), "hipMalloc frame");
+        GPU_CHECK(hipMemcpyAsync(drecon[refs[r]], J.recon + (size_t)refs[r] * fsz, fsz * 2,
+                                 hipMemcpyHostToDevice, st),
+                  "upload recon");
+      }
+  }
+  char* dres = nullptr;
+  GPU_CHECK(hipMalloc(&dres, J.L->bytes), "hipMalloc results");
+  // two slots: POC k+1 is enqueued before the host waits for POC k's copy
+  hipEvent_t e0[2], e1[2], copied[2];
+  for (int i = 0; i < 2; i++) {
+    GPU_CHECK(hipEventCreate(&e0[i]), "hipEventCreate");
+    GPU_CHECK(hipEventCreate(&e1[i]), "hipEventCreate");
+    GPU_CHECK(hipEventCreateWithFlags(&copied[i], hipEventDisableTiming), "hipEventCreate");
+  }
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> evs[2];  // per-launch timing events
+  Slab* pending = nullptr;
+  int pslot = 0;
+
+  // waits for a slot's copy, collects its kernel times, hands the slab to the writer
+  auto finish = [&](Slab* s, int slot) -> bool {
+    if (hipEventSynchronize(copied[slot]) != hipSuccess) return false;
+    float ms = 0;
+    if (J.per_launch) {
+      for (int r = 0; r < s->nrefs; r++)
+        for (int m = 0; m < 4; m++) {
+          if ((m & 1) && !(J.mode_mask & VAME_MODE_3CP)) continue;
+          if (hipEventElapsedTime(&ms, evs[slot][r * 4 + m].first, evs[slot][r * 4 + m].second))
+            return false;
+          s->pred_ns[m] += ms * 1e6f;
+        }
+    } else {
+      if (hipEventElapsedTime(&ms, e0[slot], e1[slot]) != hipSuccess) return false;
+      s->fused_ns = ms * 1e6f;
+    }
+    std::lock_guard<std::mutex> g(S->mu);
+    S->done[s->poc] = s;
+    S->cv.notify_all();
+    return true;
+  };
+
+  int k = 0;
+  for (int p : J.pocs) {
+    const int slot = k++ & 1;
+    Slab* slab = nullptr;
+    {
+      std::unique_lock<std::mutex> g(S->mu);
+      S->cv.wait(g, [&] { return S->failed || !S->pool.empty(); });
+      if (S->failed) break;
+      slab = S->pool.back();
+      S->pool.pop_back();
+    }
+    int refs[4];
+    const int nrefs = vame_ref_list(p, refs);
+    slab->poc = p;
+    slab->nrefs = nrefs;
+    const float lambda = vame_lambda(J.qp, p);
+    auto dcost = [&](int r, int m) { return (int64_t*)(dres + J.L->off_cost[r][m]); };
+    auto dcp = [&](int r, int m) { return (vame_cpmvs*)(dres + J.L->off_cp[r][m]); };
+    if (J.per_launch) {
+      // main.cpp:754-966: per refIdx, FULL_2CP, FULL_3CP, HALF_2CP, HALF_3CP
+      while (evs[slot].size() < (size_t)nrefs * 4) {
+        std::pair<hipEvent_t, hipEvent_t> e;
+        GPU_CHECK(hipEventCreate(&e.first), "hipEventCreate");
+        GPU_CHECK(hipEventCreate(&e.second), "hipEventCreate");
+        evs[slot].push_back(e);
+      }
+      for (int r = 0; r < nrefs; r++)
+        for (int m = 0; m < 4; m++) {
+          if ((m & 1) && !(J.mode_mask & VAME_MODE_3CP)) continue;
+          auto& e = evs[slot][r * 4 + m];
+          GPU_CHECK(hipEventRecord(e.first, st), "hipEventRecord");
+          VAME_CHECK(vame_affine_me(ctx, drecon[refs[r]], dorig[p], lambda, m >> 1, (m & 1) ? 3 : 2,
+                                    J.extra, (m & 1) ? dcp(r, m - 1) : nullptr, dcost(r, m),
+                                    dcp(r, m), st),
+                     "vame_affine_me");
+          GPU_CHECK(hipEventRecord(e.second, st), "hipEventRecord");
+        }
+    } else {
+      vame_poc_result out;
+      memset(&out, 0, sizeof out);
+      const uint16_t* rp[4];
+      for (int r = 0; r < nrefs; r++) {
+        rp[r] = drecon[refs[r]];
+        for (int m = 0; m < 4; m++) {
+          if ((m & 1) && !(J.mode_mask & VAME_MODE_3CP)) continue;
+          out.cost[r][m] = dcost(r, m);
+          out.cpmvs[r][m] = dcp(r, m);
+        }
+      }
+      GPU_CHECK(hipEventRecord(e0[slot], st), "hipEventRecord");
+      VAME_CHECK(vame_affine_me_poc(ctx, dorig[p], rp, nrefs, lambda, J.mode_mask, J.extra, &out, st),
+                 "vame_affine_me_poc");
+      GPU_CHECK(hipEventRecord(e1[slot], st), "hipEventRecord");
+    }
+    // stream order: this POC's kernels run after the previous POC's copy read dres
+    GPU_CHECK(hipMemcpyAsync(slab->host, dres, J.L->bytes, hipMemcpyDeviceToHost, st), "D2H");
+    GPU_CHECK(hipEventRecord(copied[slot], st), "hipEventRecord");
+    if (pending && !finish(pending, pslot)) {
+      fail(S, "waiting for results failed");
+      return;
+    }
+    pending = slab;
+    pslot = slot;
+  }
+  if (pending && !finish(pending, pslot)) {
+    fail(S, "waiting for results failed");
+    return;
+  }
+  for (int i = 0; i < 2; i++) {
+    for (auto& e : evs[i]) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+    (void)hipEventDestroy(e0[i]);
+    (void)hipEventDestroy(e1[i]);
+    (void)hipEventDestroy(copied[i]);
+  }
+  for (auto& kv : dorig) (void)hipFree(kv.second);
+  for (auto& kv : drecon) (void)hipFree(kv.second);
+  (void)hipFree(dres);
+  (void)hipStreamDestroy(st);
+  vame_destroy(ctx);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Cli c;
+  c.opts = {
+      {"DeviceIndex", 0, true, "0", "Index of the GPU device according ot clinfo command"},
+      {"QP", 'q', false, "", "Quantization parameter"},
+      {"FramesToBeEncoded", 'f', false, "", "Number of frames to be processed"},
+      {"ExtraGradientIter", 0, true, "0",
+       "Number of extra iterations during Gradient-based Affine ME"},
+      {"Resolution", 's', false, "", "Resolution of the video, in the format 1920x1080"},
+      {"OriginalFrames", 'o', false, "", "Input file for original frames samples"},
+      {"ReferenceFrames", 'r', false, "", "Input file for reference frames samples"},
+      {"CpmvLogFile", 'l', true, "", "Output files preffix with produced CPMVs"},
+      {"gpus", 0, true, "1", "number of GPUs (POCs frame-sharded over DeviceIndex..+gpus-1)"},
+      {"modes", 0, true, "all", "all = 2- and 3-CP affine, 2cp = 2-CP only"},
+      {"threads", 0, true, "0", "host threads for CSV parsing and log formatting (0 = all)"},
+      {"devices", 0, true, "", "explicit device list, e.g. 0,1,2 (overrides DeviceIndex/gpus; "
+                               "a device may repeat: several contexts on one GPU)"},
+  };
+  const int pr = parse(c, argc, argv);
+  if (pr == 1) {
+    print_help(c);
+    return 1;
+  }
+  if (pr == 2) return 1;
+  if (check_report(c) > 0) {
+    printf("Exiting after finding errors in input parameters\n");
+    return 1;
+  }
+  const bool per_launch =
+      std::find(c.flags_set.begin(), c.flags_set.end(), "per-launch") != c.flags_set.end();
+  const std::string modes = c.str("modes");
+  if (modes != "all" && modes != "2cp") {
+    printf("  [!] ERROR: --modes must be all or 2cp\n");
+    return 1;
+  }
+  const int mode_mask = modes == "all" ? (VAME_MODE_2CP | VAME_MODE_3CP) : VAME_MODE_2CP;
+  const int nthreads = c.num("threads");
+
+  print_timestamp("START HOST");
+
+  // ---- devices (the OpenCL listing of main.cpp:133-247, as HIP)
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  for (int d = 0; d < ndev; d++) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, d) != hipSuccess) continue;
+    printf("GPU %d\n\t%s (%s)\n", d, p.name, p.gcnArchName);
+  }
+  std::vector<int> devices;
+  if (!c.str("devices").empty()) {
+    std::stringstream ss(c.str("devices"));
+    for (std::string t; std::getline(ss, t, ',');) devices.push_back(atoi(t.c_str()));
+  } else {
+    for (int g = 0; g < std::max(1, c.num("gpus")); g++) devices.push_back(c.num("DeviceIndex") + g);
+  }
+  const int ngpu = (int)devices.size();
+  for (int d : devices)
+    if (d < 0 || d >= ndev) {
+      printf("Incorrect GPU index. Only %d GPUs are detected\n", ndev);
+      return 0;
+    }
+  for (int d : devices) {
+    hipDeviceProp_t p;
+    (void)hipGetDeviceProperties(&p, d);
+    printf("COMPUTING ON GPU %d\n", d);
+    printf("-- Max compute units %d\n", p.multiProcessorCount);
+  }
+
+  // ---- resolution (main.cpp:285-306)
+  const std::string res = c.str("Resolution");
+  std::vector<std::string> tok;
+  {
+    std::stringstream ss(res);
+    for (std::string t; std::getline(ss, t, 'x');) tok.push_back(t);
+  }
+  if (tok.size() != 2) {
+    printf("  [!] ERROR: Input resolution \"%s\" not set properly\n", res.c_str());
+    return 0;
+  }
+  const int W = atoi(tok[0].c_str()), H = atoi(tok[1].c_str());
+  const int nCtus = vame_num_ctus(W, H);
+  if (nCtus == 0) {
+    printf("[!] ERROR: Unsupported resolution %dx%d\n", W, H);
+    printf("Supported resolutions are:\n");
+    const int rs[5][2] = {{3840, 2160}, {1920, 1080}, {1280, 720}, {832, 480}, {416, 240}};
+    for (auto& r : rs) printf("  %dx%d\n", r[0], r[1]);
+    return 0;
+  }
+  const int N = c.num("FramesToBeEncoded"), qp = c.num("QP"), extra = c.num("ExtraGradientIter");
+  const std::string prefix = c.str("CpmvLogFile");
+  if (N <= 0) {
+    printf("  [!] ERROR: FramesToBeEncoded must be positive\n");
+    return 1;
+  }
+  if (vame_lambda(qp, 1) < 0 || vame_lambda(qp, 8) < 0) {
+    printf("  [!] ERROR: QP %d outside the lambda table\n", qp);
+    return 1;
+  }
+
+  test_references(N, qp);
+
+  // ---- inputs (main.cpp:308-330)
+  const size_t fsz = (size_t)W * H;
+  std::vector<uint16_t> orig(fsz * N), recon(fsz * N);
+  {
+    FILE* a = fopen(c.str("OriginalFrames").c_str(), "r");
+    FILE* b = fopen(c.str("ReferenceFrames").c_str(), "r");
+    if (!a || !b) {
+      perror("error while opening samples files");
+      return 1;
+    }
+    fclose(a);
+    fclose(b);
+  }
+  print_timestamp("START READ .csv");
+  if (vame_read_frames(c.str("ReferenceFrames").c_str(), W, H, N, recon.data(), nthreads) ||
+      vame_read_frames(c.str("OriginalFrames").c_str(), W, H, N, orig.data(), nthreads)) {
+    printf("  [!] ERROR: could not read %d frames of %dx%d from the sample files\n", N, W, H);
+    return 1;
+  }
+  print_timestamp("FINISHED READ .csv");
+
+  printf("Removing older outputs with identical names...\n");  // main.cpp:469 -> :1548
+  vame_log_remove_old(prefix.c_str());
+
+  // ---- shard POCs 1..N over the devices: contiguous blocks balanced by pair count
+  print_timestamp("START ALLOCATE MEMORY");
+  const Layout L(nCtus);
+  Shared S;
+  const int nslabs = std::max(4, 3 * ngpu);
+  std::vector<Slab> slabs(nslabs);
+  for (auto& s : slabs) {
+    if (hipHostMalloc((void**)&s.host, L.bytes, hipHostMallocDefault) != hipSuccess) {
+      printf("  [!] ERROR: pinned host allocation of %zu bytes failed\n", L.bytes);
+      return 1;
+    }
+    S.pool.push_back(&s);
+  }
+  std::vector<Job> jobs(ngpu);
+  {
+    long total = 0;
+    for (int p = 1; p <= N; p++) total += std::min(4, p);
+    long acc = 0;
+    int g = 0;
+    for (int p = 1; p <= N; p++) {
+      // move to the next device once this one holds its share of (POC, ref) pairs
+      if (g < ngpu - 1 && acc >= total * (g + 1) / ngpu) g++;
+      jobs[g].pocs.push_back(p);
+      acc += std::min(4, p);
+    }
+  }
+  print_timestamp("FINISH ALLOCATE MEMORY");
+
+  print_timestamp("START GPU KERNEL");
+  const double t0 = now_s();
+  std::vector<std::thread> workers;
+  for (int g = 0; g < ngpu; g++) {
+    Job& j = jobs[g];
+    j.device = devices[g];
+    j.W = W;
+    j.H = H;
+    j.nCtus = nCtus;
+    j.qp = qp;
+    j.extra = extra;
+    j.mode_mask = mode_mask;
+    j.per_launch = per_launch;
+    j.orig = orig.data();
+    j.recon = recon.data();
+    j.L = &L;
+    j.S = &S;
+    if (!j.pocs.empty()) workers.emplace_back(gpu_worker, j);
+  }
+
+  // ---- writer: POCs in order (main.cpp:954-958 -> main_aux_functions.h:387-525)
+  float pred_ns[4] = {0, 0, 0, 0}, fused_ns = 0;
+  long long log_bytes = 0;
+  bool ok = true;
+  for (int p = 1; p <= N && ok; p++) {
+    Slab* s = nullptr;
+    {
+      std::unique_lock<std::mutex> g(S.mu);
+      S.cv.wait(g, [&] { return S.failed || S.done.count(p); });
+      if (S.failed) {
+        ok = false;
+        break;
+      }
+      s = S.done[p];
+      S.done.erase(p);
+    }
+    const float lambda = vame_lambda(qp, p);
+    for (int r = 0; r < s->nrefs; r++) {
+      printf("POC   %d  RefIdx  %d  -> lambda %f\n", p, r, (double)lambda);
+      for (int m = 0; m < 4; m++) {
+        if ((m & 1) && !(mode_mask & VAME_MODE_3CP)) continue;
+        printf("Reporting results POC=%d refIdx=%d PredType=%d\n", p, r, m);
+        if (prefix.empty()) continue;
+        if (p == 1 && r == 0) {
+          printf("Writing headers\n");
+          if (vame_log_write_headers(prefix.c_str(), m)) {
+            printf("  [!] ERROR: cannot create the log files %s_*\n", prefix.c_str());
+            ok = false;
+            break;
+          }
+        }
+        const long long nb =
+            vame_log_append(prefix.c_str(), m, W, H, p, r, (const int64_t*)(s->host + L.off_cost[r][m]),
+                            (const vame_cpmvs*)(s->host + L.off_cp[r][m]), nthreads);
+        if (nb < 0) {
+          printf("  [!] ERROR: writing the log files %s_* failed\n", prefix.c_str());
+          ok = false;
+          break;
+        }
+        log_bytes += nb;
+      }
+      if (!ok) break;
+    }
+    for (int m = 0; m < 4; m++) pred_ns[m] += s->pred_ns[m];
+    fused_ns += s->fused_ns;
+    memset(s->pred_ns, 0, sizeof s->pred_ns);
+    s->fused_ns = 0;
+    std::lock_guard<std::mutex> g(S.mu);
+    S.pool.push_back(s);
+    S.cv.notify_all();
+  }
+  if (!ok) {
+    std::lock_guard<std::mutex> g(S.mu);
+    S.failed = true;
+    S.cv.notify_all();
+  }
+  for (auto& t : workers) t.join();
+  fflush(stdout);
+  if (!S.error.empty() || !ok) {
+    printf("  [!] ERROR: %s\n", S.error.empty() ? "log writer failed" : S.error.c_str());
+    return 1;
+  }
+  print_timestamp("FINISH GPU KERNEL");
+  const double overall = now_s() - t0;
+
+  // main_aux_functions.h:1416-1446 reportTimingResults (ns; float like the reference)
+  printf("=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=\n");
+  printf("TIMING RESULTS (nanoseconds)\n");
+  printf("FULL_2CP_EXEC,%f\n", (double)pred_ns[0]);
+  printf("FULL_3CP_EXEC,%f\n", (double)pred_ns[1]);
+  printf("HALF_2CP_EXEC,%f\n", (double)pred_ns[2]);
+  printf("HALF_3CP_EXEC,%f\n", (double)pred_ns[3]);
+  if (!per_launch) printf("FUSED_POC_EXEC,%f\n", (double)fused_ns);
+  printf("TOTAL_EXEC_TIME(%dx),%f\n", N,
+         (double)(pred_ns[0] + pred_ns[1] + pred_ns[2] + pred_ns[3] + fused_ns));
+  printf("OVERALL(%dx),%f\n", N, (double)(float)overall);
+  printf("LOG_BYTES,%lld\n", log_bytes);
+  printf("=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=\n\n");
+
+  for (auto& s : slabs) (void)hipHostFree(s.host);
+  print_timestamp("FINISH HOST");
+  return 0;
+}

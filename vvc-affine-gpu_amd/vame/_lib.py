@@ -13,7 +13,8 @@ EXPORTS = (
     "vame_create", "vame_destroy", "vame_affine_me", "vame_affine_me_poc", "vame_num_ctus",
     "vame_cus_per_ctu", "vame_num_groups", "vame_group_geometry", "vame_lambda", "vame_poc_qp",
     "vame_ref_list", "vame_strerror", "vame_last_hip_error", "vame_version", "vame_set_timing",
-    "vame_get_timing",
+    "vame_get_timing", "vame_read_frames", "vame_log_remove_old", "vame_log_write_headers",
+    "vame_log_append", "vame_log_file_count",
 )
 
 
@@ -55,6 +56,13 @@ def lib():
         L.vame_set_timing.argtypes = [P, I]
         L.vame_get_timing.argtypes = [P, I, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_int), I]
+        C = ctypes.c_char_p
+        L.vame_read_frames.argtypes = [C, I, I, I, P, I]
+        L.vame_log_remove_old.argtypes = [C]
+        L.vame_log_write_headers.argtypes = [C, I]
+        L.vame_log_append.argtypes = [C, I, I, I, I, I, P, P, I]
+        L.vame_log_append.restype = ctypes.c_longlong
+        L.vame_log_file_count.argtypes = [I]
         _lib = L
     return _lib
 
