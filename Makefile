@@ -26,6 +26,10 @@ ABLATE_SET ?= 1 2 4 6 7 8 11 13 14 15 16 32
 ablate:
 	@mkdir -p $(LIBDIR)
 	for a in $(ABLATE_SET); do $(HIPCC) $(HIPFLAGS) -DVAME_ABLATE=$$a -shared -o $(LIBDIR)/libvame_ablate$$a.so $(LIB_SRCS) || exit 1; done
+# experiment builds: make variant NAME=x DEFS="-DFOO=1" -> lib/libvame_x.so
+variant:
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(LIBDIR)/libvame_$(NAME).so $(LIB_SRCS)
 # profiling-only build with per-phase shader-clock counters: make phase
 phase:
 	@mkdir -p $(LIBDIR)
@@ -53,4 +57,4 @@ clean:
 	rm -rf $(LIBDIR) $(BINDIR)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all lib cli oracle clean resource-usage ablate phase
+.PHONY: all lib cli oracle clean resource-usage ablate phase variant

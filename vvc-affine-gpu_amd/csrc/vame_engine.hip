@@ -14,6 +14,10 @@
 #include "../../include/vame.h"
 #include "vame_kernel.h"
 
+#ifndef VAME_BIG_STREAM
+#define VAME_BIG_STREAM 0
+#endif
+
 using namespace vame;
 
 static_assert(sizeof(vame_cpmvs) == 28, "Cpmvs layout (typedef.h)");
@@ -228,39 +232,47 @@ int time_end(vame_ctx* c, int cls, hipStream_t s) {
 
 int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
            hipStream_t stream) {
-  // 128-class items (big LDS, 1 workgroup per CU) go first on a side stream so
-  // they overlap with the quadrant items instead of forming a tail.
+  // 128-class items (big LDS, 1 workgroup per CU) and quadrant items run on
+  // two streams so they overlap; VAME_BIG_STREAM picks which one the 128-class
+  // kernel is issued on (0: side stream, after an event; 1: caller's stream,
+  // first, with the quadrant kernel on the side stream).
   if (VAME_ABLATE & 16) bigItems = false;  // timing-only builds
   if (VAME_ABLATE & 32) quadFull = quadHalf = false;
   const bool fork = bigItems && (quadFull || quadHalf);
-  if (bigItems) {
+  hipStream_t sBig = stream, sQuad = stream;
+  if (fork) {
+    VAME_HIP(hipEventRecord(c->evFork, stream));
+    VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
+    if (VAME_BIG_STREAM) sQuad = c->side; else sBig = c->side;
+  }
+  auto big = [&]() -> int {
     KParams kb = kp;
     kb.items = c->dBig;
     kb.nItems = c->nBig;
     const unsigned grid = (unsigned)(kb.nItems * kb.nCtus * kb.nRefs);
-    hipStream_t s = stream;
-    if (fork) {
-      VAME_HIP(hipEventRecord(c->evFork, stream));
-      VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
-      s = c->side;
-    }
-    VAME_TRY(time_begin(c, 1, s));
-    hipLaunchKernelGGL(affine_me_ctu, dim3(grid), dim3(Cfg<128>::THREADS), 0, s, kb);
+    VAME_TRY(time_begin(c, 1, sBig));
+    hipLaunchKernelGGL(affine_me_ctu, dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig, kb);
     VAME_HIP(hipGetLastError());
-    VAME_TRY(time_end(c, 1, s));
-    if (fork) VAME_HIP(hipEventRecord(c->evJoin, s));
-  }
-  if (quadFull || quadHalf) {
+    VAME_TRY(time_end(c, 1, sBig));
+    return VAME_OK;
+  };
+  auto quad = [&]() -> int {
     KParams kq = kp;
     kq.items = quadFull ? c->dQuad : c->dQuad + c->nQuadFull;
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
     const unsigned grid = (unsigned)(kq.nItems * kq.nCtus * kq.nRefs);
-    VAME_TRY(time_begin(c, 0, stream));
-    hipLaunchKernelGGL(affine_me_quad, dim3(grid), dim3(Cfg<64>::THREADS), 0, stream, kq);
+    VAME_TRY(time_begin(c, 0, sQuad));
+    hipLaunchKernelGGL(affine_me_quad, dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad, kq);
     VAME_HIP(hipGetLastError());
-    VAME_TRY(time_end(c, 0, stream));
+    VAME_TRY(time_end(c, 0, sQuad));
+    return VAME_OK;
+  };
+  if (bigItems) VAME_TRY(big());
+  if (quadFull || quadHalf) VAME_TRY(quad());
+  if (fork) {
+    VAME_HIP(hipEventRecord(c->evJoin, c->side));
+    VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
   }
-  if (fork) VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
   return VAME_OK;
 }
 

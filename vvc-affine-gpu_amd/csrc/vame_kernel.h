@@ -98,6 +98,12 @@ struct KParams {
 #ifndef VAME_ABLATE
 #define VAME_ABLATE 0
 #endif
+// VAME_DUP (timing-only builds, results stay correct): run a phase twice to
+// price it in throughput terms: bit 0 prediction, bit 1 gradient, bit 2
+// equation reduction, bit 3 tile staging.
+#ifndef VAME_DUP
+#define VAME_DUP 0
+#endif
 
 // VAME_PHASE_TIMING (profiling-only builds, libvame_phase.so): every wave sums
 // the shader clock spent per phase and adds it to g_phase_cycles at exit.
@@ -784,6 +790,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   __shared__ CuSlot s_cu[kMaxCu];
   __shared__ WaveDesc s_wave[kMaxWaves];
   __shared__ int s_hdr[4];
+  __shared__ long long s_dup[(VAME_DUP & 4) ? kNumMom : 1];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
@@ -821,7 +828,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 
   // ---- stage the reference region (+margin) into LDS, clamp-to-edge padded:
   // 16-byte chunks, every load of a thread issued before its first LDS store
-  {
+  for (int dupS = 0; dupS < ((VAME_DUP & 8) ? 2 : 1); dupS++) {
     constexpr int CPR = C::TILE / 8;  // chunks per tile row
     constexpr int NCH = C::TILE * CPR;
     constexpr int PER = (NCH + C::THREADS - 1) / C::THREADS;
@@ -961,6 +968,15 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
         satdLane = predict_sb<C::TILE, C::TP>(f, sxp, syp, gp, s_tile, tx0, ty0, ref, cur, W, H,
                                               s_coef, Pr, Og);
+        if (VAME_DUP & 1) {
+          MvField f2 = f;
+          opaque(f2.bx);
+          uint2 P2[4], O2[4];
+          int s2 = predict_sb<C::TILE, C::TP>(f2, sxp, syp, gp, s_tile, tx0, ty0, ref, cur, W, H,
+                                              s_coef, P2, O2);
+          s2 += (int)(P2[0].x ^ P2[3].y ^ O2[1].x);
+          asm volatile("" ::"v"(s2));
+        }
       }
       // extended rows (neighbour columns by DPP), edge rows published for the
       // sub-blocks above and below
@@ -1014,6 +1030,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           int sxg = sx, syg = sy;
           opaque_geo(gg, sxg, syg);
           grad_sb(sxg, syg, gg, X, Og, S);
+          if (VAME_DUP & 2) {
+            int S2[5];
+            int sxd = sxg;
+            opaque(sxd);
+            grad_sb(sxd, syg, gg, X, Og, S2);
+            asm volatile("" ::"v"(S2[0] ^ S2[1] ^ S2[2] ^ S2[3] ^ S2[4]));
+          }
         }
         if (!(VAME_ABLATE & 4)) {
           long long* dst = s_val[myCu < 0 ? 0 : myCu];
@@ -1021,6 +1044,14 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             reduce_equations<2>(S, sx + 2, sy + 2, logS, leader, coop, dst);
           else
             reduce_equations<3>(S, sx + 2, sy + 2, logS, leader, coop, dst);
+          if constexpr ((VAME_DUP & 4) != 0) {
+            int ud = sx + 2;
+            opaque(ud);
+            if (ncp == 2)
+              reduce_equations<2>(S, ud, sy + 2, logS, leader, coop, s_dup);
+            else
+              reduce_equations<3>(S, ud, sy + 2, logS, leader, coop, s_dup);
+          }
         }
       }
       phase_sync(coop);
