@@ -539,19 +539,22 @@ __device__ __forceinline__ void grad_sb(int sx, int sy, const Geo& g, const uint
 // reduced values V; column N is the right-hand side (<< 3, affine.cl:705).
 // Integer sums below 2^53 convert to double exactly.
 template <int NCP>
-__device__ __forceinline__ double eq_element(const long long* V, int r, int c) {
+__device__ __forceinline__ long long reduced_value(const long long* V, int i, bool coop);
+
+template <int NCP>
+__device__ __forceinline__ double eq_element(const long long* V, int r, int c, bool coop) {
   if constexpr (NCP == 2) {
-    if (c == 4) return (double)(V[10 + r] * 8);
+    if (c == 4) return (double)(reduced_value<2>(V, 10 + r, coop) * 8);
     const int lo = min(r, c), hi = max(r, c);  // symmetric: A00 A01 A02 A03 A11 A12 A13 A22 A23 A33
-    return (double)V[lo == 0 ? hi : lo == 1 ? 3 + hi : lo == 2 ? 5 + hi : 9];
+    return (double)reduced_value<2>(V, lo == 0 ? hi : lo == 1 ? 3 + hi : lo == 2 ? 5 + hi : 9, coop);
   } else {
     // regressor r = (gradient t: 0 x / 1 y, monomial m: 0 1 / 1 u / 2 v):
     // gx, u gx, gy, u gy, v gx, v gy (affine.cl:684-689)
     const int tr = (r == 2 || r == 3 || r == 5) ? 1 : 0, mr = (r == 1 || r == 3) ? 1 : (r >= 4 ? 2 : 0);
-    if (c == 6) return (double)(V[18 + 3 * tr + mr] * 8);
+    if (c == 6) return (double)(reduced_value<3>(V, 18 + 3 * tr + mr, coop) * 8);
     const int tc = (c == 2 || c == 3 || c == 5) ? 1 : 0, mc = (c == 1 || c == 3) ? 1 : (c >= 4 ? 2 : 0);
     const int prod = mr == 0 ? mc : mc == 0 ? mr : (mr == 1 && mc == 1) ? 3 : (mr == 2 && mc == 2) ? 5 : 4;
-    return (double)V[6 * (tr + tc) + prod];
+    return (double)reduced_value<3>(V, 6 * (tr + tc) + prod, coop);
   }
 }
 
@@ -649,7 +652,7 @@ __device__ __forceinline__ void seg_solve(long long* V, double* M, int li, int L
                                           bool coop, int lw, int lh, double dd[6]) {
   constexpr int N = 2 * NCP, NC = N + 1;
   if (act) {
-    for (int e = li; e < N * NC; e += Ls) M[e] = eq_element<NCP>(V, e / NC, e % NC);
+    for (int e = li; e < N * NC; e += Ls) M[e] = eq_element<NCP>(V, e / NC, e % NC, coop);
     if (coop && li < kNumMom) V[li] = 0;  // cooperative items accumulate with atomics
   }
   wave_sync();
@@ -739,41 +742,202 @@ __device__ __forceinline__ int seg_sum_c(int v) {
   return v;
 }
 
-// Reduction of a CU's equations over its sub-blocks (one per lane): the last
-// lane of every segment stores (autonomous) or adds (cooperative) the
-// segment's sums into the CU's LDS row.  Each int64 value x is reduced as two
-// int32 halves, x = hi * 2^24 + lo with lo in [0, 2^24): |x| < 2^44, so over
-// at most 64 lanes sum(lo) < 2^30 and |sum(hi)| < 2^26 -- exact.
+// Reduction of a CU's equations over its sub-blocks (one per lane), as a
+// transposing butterfly.  Each int64 value x is split into two int32 halves,
+// x = hi * 2^24 + lo with lo in [0, 2^24): |x| < 2^44, so over at most 64
+// lanes sum(lo) < 2^30 and |sum(hi)| < 2^26 -- exact.  The K = 2 * NV halves
+// of every lane are then summed over the segment (the CU's lanes in this
+// wave) by halving exchanges: at a step over lane bit b, the lanes with bit b
+// clear keep the first half of their values and send the second half to the
+// partner lane (lane ^ 2^b), which keeps the second half -- so each step
+// halves the values a lane holds and doubles the lanes they are summed over.
+// Steps run in order of cost: bit 5 (v_permlane32_swap, 2 instructions per
+// exchanged pair), bit 4 (v_permlane16_swap), bit 3 (DPP row_ror:8), bits 1
+// and 0 (DPP quad_perm), bit 2 (two banked DPP moves).  After the last step
+// every half is held, fully summed, by exactly one lane of the segment, which
+// stores it (autonomous items: int32 slots) or adds it (cooperative items:
+// int64 LDS atomics across waves).  Integer sums: the order is free.
+template <int M>
+struct HalfVals {
+  int v[M];
+};
+
+// lane-bit masks of the wave (the exchange partner's bit), wave-uniform
+__device__ __forceinline__ bool lane_bit(int b) { return (__lane_id() >> b) & 1; }
+
+// One exchange over lane bit B via DPP: returns keep + partner(send).
+template <int B>
+__device__ __forceinline__ int xchg_dpp(int keep, int send) {
+  if constexpr (B == 3) return keep + dpp32<0x128, 0xF>(send);  // row_ror:8 == lane ^ 8
+  if constexpr (B == 1) return keep + dpp32<0x4E, 0xF>(send);   // quad_perm [2,3,0,1]
+  if constexpr (B == 0) return keep + dpp32<0xB1, 0xF>(send);   // quad_perm [1,0,3,2]
+  // B == 2: lane ^ 4 = row_shl:4 into banks 0/2, row_shr:4 into banks 1/3
+  int r = __builtin_amdgcn_update_dpp(0, send, 0x104, 0xF, 0x5, false);
+  r = __builtin_amdgcn_update_dpp(r, send, 0x114, 0xF, 0xA, false);
+  return keep + r;
+}
+
+// Halving step over lane bit B on the first M values of x (the rest unused):
+// afterwards x[0 .. ceil(M/2)) holds this lane's kept half.
+template <int B, int M>
+__device__ __forceinline__ void halve(int* x) {
+  constexpr int H = (M + 1) / 2;
+  if constexpr (B >= 4) {
+#pragma unroll
+    for (int j = 0; j < H; j++) {
+      const unsigned a = (unsigned)x[j], b = j + H < M ? (unsigned)x[j + H] : 0u;
+      // bit 5: lanes 0-31 end with a summed over (l, l^32), lanes 32-63 with b
+      const auto r = B == 5 ? __builtin_amdgcn_permlane32_swap(a, b, false, false)
+                            : __builtin_amdgcn_permlane16_swap(a, b, false, false);
+      x[j] = (int)(r[0] + r[1]);
+    }
+  } else {
+    const bool beta = lane_bit(B);
+#pragma unroll
+    for (int j = 0; j < H; j++) {
+      const int a = x[j], b = j + H < M ? x[j + H] : 0;
+      x[j] = xchg_dpp<B>(beta ? b : a, beta ? a : b);
+    }
+  }
+}
+
+constexpr int ceil_half(int m) { return (m + 1) / 2; }
+
+// Step schedule per segment size: bits (in order) and the count after them.
+template <int LOGS, int K>
+struct Schedule {
+  // bit order: 5 4 3 1 0 2 restricted to bits < LOGS
+  static constexpr int NB = LOGS;
+  static constexpr int bit(int i) {
+    constexpr int all[6] = {5, 4, 3, 1, 0, 2};
+    int n = 0;
+    for (int k = 0; k < 6; k++)
+      if (all[k] < LOGS) {
+        if (n == i) return all[k];
+        n++;
+      }
+    return -1;
+  }
+};
+
+// Runs the halving steps while the count is > 1; returns (through x) the
+// values and reports how many halving steps ran.  A remaining segment bit
+// after the count reached 1 becomes a plain sum (valid in the lanes whose bit
+// is set).
+template <int LOGS, int STEP, int M>
+__device__ __forceinline__ void butterfly(int* x) {
+  if constexpr (STEP < LOGS) {
+    constexpr int B = Schedule<LOGS, M>::bit(STEP);
+    if constexpr (M > 1) {
+      halve<B, M>(x);
+      butterfly<LOGS, STEP + 1, ceil_half(M)>(x);
+    } else {
+      static_assert(B == 2, "plain steps only on bit 2");
+      x[0] += dpp32<0x114, 0xF>(x[0]);  // row_shr:4: banks 1/3 hold the sum
+      butterfly<LOGS, STEP + 1, M>(x);
+    }
+  }
+}
+
+// Count left per lane after the schedule, and whether a plain step ran.
+template <int LOGS, int M, int STEP = 0>
+struct Final {
+  static constexpr int count() {
+    int m = M;
+    for (int i = 0; i < LOGS; i++)
+      if (m > 1) m = ceil_half(m);
+    return m;
+  }
+  static constexpr bool plain() {
+    int m = M, halvings = 0;
+    for (int i = 0; i < LOGS; i++)
+      if (m > 1) {
+        m = ceil_half(m);
+        halvings++;
+      }
+    return halvings < LOGS;
+  }
+};
+
+// Window of value indices a lane holds after the schedule: [off, off + count),
+// valid below `limit` (the upper half of an odd count carries a zero pad).
+template <int LOGS, int K>
+__device__ __forceinline__ void held_window(int lidx, int& off, int& limit) {
+  off = 0;
+  limit = K;
+  int m = K;
+#pragma unroll
+  for (int i = 0; i < LOGS; i++) {
+    if (m <= 1) break;
+    const int b = Schedule<LOGS, K>::bit(i);
+    const int h = ceil_half(m);
+    if ((lidx >> b) & 1) {
+      off += h;
+    } else {
+      limit = off + h;
+    }
+    m = h;
+  }
+}
+
 template <int NCP, int LOGS, bool COOP>
-__device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int v, bool leader,
+__device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int v, bool owner,
                                                    long long* dst) {
   constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
+  constexpr int K = 2 * NV;
+  int x[K];
 #pragma unroll
   for (int i = 0; i < NV; i++) {
-    const long long x = eq_value<NCP>(i, S, u, v);
-    const int lo = seg_sum_c<LOGS>((int)((unsigned)x & 0xFFFFFFu));
-    const int hi = seg_sum_c<LOGS>((int)(x >> 24));
-    if (leader) {
-      const long long r = (long long)hi * (1ll << 24) + (long long)(unsigned)lo;
-      if (COOP)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&dst[i]), (unsigned long long)r);
-      else
-        dst[i] = r;
+    const long long e = eq_value<NCP>(i, S, u, v);
+    x[i] = (int)((unsigned)e & 0xFFFFFFu);
+    x[NV + i] = (int)(e >> 24);
+  }
+  butterfly<LOGS, 0, K>(x);
+  constexpr int CNT = Final<LOGS, K>::count();
+  const int lidx = __lane_id() & ((1 << LOGS) - 1);
+  int off, limit;
+  held_window<LOGS, K>(lidx, off, limit);
+  bool ok = owner;
+  if constexpr (Final<LOGS, K>::plain()) ok = ok && ((lidx >> 2) & 1);
+  if (ok) {
+#pragma unroll
+    for (int j = 0; j < CNT; j++) {
+      const int idx = off + j;
+      if (idx < limit) {
+        if constexpr (COOP) {
+          const unsigned long long add =
+              idx < NV ? (unsigned long long)(unsigned)x[j]
+                       : (unsigned long long)((long long)x[j] * (1ll << 24));
+          atomicAdd(reinterpret_cast<unsigned long long*>(&dst[idx < NV ? idx : idx - NV]), add);
+        } else {
+          reinterpret_cast<int*>(dst)[idx] = x[j];  // int32 slots: lo[0..NV), hi[NV..2NV)
+        }
+      }
     }
   }
 }
 template <int NCP>
 __device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v, int logS,
-                                                 bool leader, bool coop, long long* dst) {
+                                                 bool owner, bool coop, long long* dst) {
   if (coop) {  // cooperative items: whole-wave segments, partial sums meet in LDS atomics
-    reduce_equations_c<NCP, 6, true>(S, u, v, leader, dst);
+    reduce_equations_c<NCP, 6, true>(S, u, v, owner, dst);
     return;
   }
   switch (logS) {  // wave-uniform; autonomous waves hold CUs of 16, 32 or 64 sub-blocks
-    case 4: reduce_equations_c<NCP, 4, false>(S, u, v, leader, dst); break;
-    case 5: reduce_equations_c<NCP, 5, false>(S, u, v, leader, dst); break;
-    default: reduce_equations_c<NCP, 6, false>(S, u, v, leader, dst); break;
+    case 4: reduce_equations_c<NCP, 4, false>(S, u, v, owner, dst); break;
+    case 5: reduce_equations_c<NCP, 5, false>(S, u, v, owner, dst); break;
+    default: reduce_equations_c<NCP, 6, false>(S, u, v, owner, dst); break;
   }
+}
+
+// Reduced value i of a CU: int64 (cooperative items) or int32 halves
+// (autonomous items, see reduce_equations_c).
+template <int NCP>
+__device__ __forceinline__ long long reduced_value(const long long* V, int i, bool coop) {
+  constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
+  if (coop) return V[i];
+  const int* V32 = reinterpret_cast<const int*>(V);
+  return (long long)V32[NV + i] * (1ll << 24) + (long long)(unsigned)V32[i];
 }
 
 template <int REGION>
@@ -1041,16 +1205,16 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         if (!(VAME_ABLATE & 4)) {
           long long* dst = s_val[myCu < 0 ? 0 : myCu];
           if (ncp == 2)
-            reduce_equations<2>(S, sx + 2, sy + 2, logS, leader, coop, dst);
+            reduce_equations<2>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
           else
-            reduce_equations<3>(S, sx + 2, sy + 2, logS, leader, coop, dst);
+            reduce_equations<3>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
           if constexpr ((VAME_DUP & 4) != 0) {
             int ud = sx + 2;
             opaque(ud);
             if (ncp == 2)
-              reduce_equations<2>(S, ud, sy + 2, logS, leader, coop, s_dup);
+              reduce_equations<2>(S, ud, sy + 2, logS, myCu >= 0, coop, s_dup);
             else
-              reduce_equations<3>(S, ud, sy + 2, logS, leader, coop, s_dup);
+              reduce_equations<3>(S, ud, sy + 2, logS, myCu >= 0, coop, s_dup);
           }
         }
       }
