@@ -368,6 +368,53 @@ __device__ __forceinline__ void filter_rows_global(const uint16_t* __restrict__ 
   }
 }
 
+// xCalcHADs4x4 with the JVET_R0164 DC weighting (aux_functions.cl:1940-2043)
+// on packed int16 pairs: the residual o - p is within +-1023, so every stage
+// of the 4x4 Hadamard stays within +-16368 and the packed 16-bit adds are
+// exact.  Rows are transformed first (elementwise on row vectors), then each
+// row vector (c0,c1)(c2,c3); the outputs are the same 16 Walsh-Hadamard
+// coefficients as the reference's butterfly (in another order -- the sum of
+// magnitudes does not depend on it), the DC term being the first lane of row
+// vector 0.  |.| sums run on v_dot2 against (1,1).
+__device__ __forceinline__ int satd_4x4(const uint2 (&O)[4], const uint2 (&P)[4]) {
+  short2v a[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    a[r][0] = as_s2(O[r].x) - as_s2(P[r].x);
+    a[r][1] = as_s2(O[r].y) - as_s2(P[r].y);
+  }
+  short2v d[4][2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const short2v m0 = a[0][k] + a[3][k], m1 = a[1][k] + a[2][k];
+    const short2v m2 = a[1][k] - a[2][k], m3 = a[0][k] - a[3][k];
+    d[0][k] = m0 + m1;
+    d[1][k] = m2 + m3;
+    d[2][k] = m0 - m1;
+    d[3][k] = m3 - m2;
+  }
+  const short2v pm = {1, -1}, z = {0, 0};
+  int sum = 0, dc = 0;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const short2v X = d[r][0], Ys = __builtin_shufflevector(d[r][1], d[r][1], 1, 0);
+    const short2v mm = X + Ys, nn = X - Ys;  // (c0+c3, c1+c2), (c0-c3, c1-c2)
+    // (u + v, u - v) of each pair, one v_pk_mad_i16 with op_sel
+    const short2v e0 = __builtin_shufflevector(mm, mm, 1, 1) * pm + __builtin_shufflevector(mm, mm, 0, 0);
+    const short2v e1 = __builtin_shufflevector(nn, nn, 1, 1) * pm + __builtin_shufflevector(nn, nn, 0, 0);
+    const short2v a0 = __builtin_elementwise_max(e0, z - e0), a1 = __builtin_elementwise_max(e1, z - e1);
+    if (r == 0) {
+      dc = (unsigned short)a0[0];
+      sum = dot2(as_u(a0), 0x00010000u, sum);
+    } else {
+      sum = dot2(as_u(a0), 0x00010001u, sum);
+    }
+    sum = dot2(as_u(a1), 0x00010001u, sum);
+  }
+  sum += dc >> 2;
+  return (sum + 1) >> 1;
+}
+
 // One 4x4 sub-block: affine MV (affine.cl:215-252), 9x9 window with
 // clamp-to-edge (affine.cl:254-326), separable 6-tap filter (aux_functions.cl
 // :1096-1239, PROF off), SATD against the original (aux_functions.cl:1940-2043).
@@ -413,44 +460,12 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   for (int r = 0; r < 4; r++)
 #pragma unroll
     for (int c = 0; c < 4; c++) pr[r][c] = clampi(acc[r][c] >> 10, 0, 1023);  // clipPel
-  int diff[16];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     P[r].x = pack16(pr[r][0], pr[r][1]);
     P[r].y = pack16(pr[r][2], pr[r][3]);
-    const uint2 o = O[r];
-    diff[r * 4 + 0] = (int)(o.x & 0xFFFF) - pr[r][0];
-    diff[r * 4 + 1] = (int)(o.x >> 16) - pr[r][1];
-    diff[r * 4 + 2] = (int)(o.y & 0xFFFF) - pr[r][2];
-    diff[r * 4 + 3] = (int)(o.y >> 16) - pr[r][3];
   }
-  // xCalcHADs4x4 (aux_functions.cl:1940-2043, JVET_R0164 DC weighting)
-  int m[16], d[16];
-  m[0] = diff[0] + diff[12]; m[1] = diff[1] + diff[13];
-  m[2] = diff[2] + diff[14]; m[3] = diff[3] + diff[15];
-  m[4] = diff[4] + diff[8];  m[5] = diff[5] + diff[9];
-  m[6] = diff[6] + diff[10]; m[7] = diff[7] + diff[11];
-  m[8] = diff[4] - diff[8];  m[9] = diff[5] - diff[9];
-  m[10] = diff[6] - diff[10]; m[11] = diff[7] - diff[11];
-  m[12] = diff[0] - diff[12]; m[13] = diff[1] - diff[13];
-  m[14] = diff[2] - diff[14]; m[15] = diff[3] - diff[15];
-  d[0] = m[0] + m[4];  d[1] = m[1] + m[5];  d[2] = m[2] + m[6];  d[3] = m[3] + m[7];
-  d[4] = m[8] + m[12]; d[5] = m[9] + m[13]; d[6] = m[10] + m[14]; d[7] = m[11] + m[15];
-  d[8] = m[0] - m[4];  d[9] = m[1] - m[5];  d[10] = m[2] - m[6]; d[11] = m[3] - m[7];
-  d[12] = m[12] - m[8]; d[13] = m[13] - m[9]; d[14] = m[14] - m[10]; d[15] = m[15] - m[11];
-  m[0] = d[0] + d[3];  m[1] = d[1] + d[2];  m[2] = d[1] - d[2];  m[3] = d[0] - d[3];
-  m[4] = d[4] + d[7];  m[5] = d[5] + d[6];  m[6] = d[5] - d[6];  m[7] = d[4] - d[7];
-  m[8] = d[8] + d[11]; m[9] = d[9] + d[10]; m[10] = d[9] - d[10]; m[11] = d[8] - d[11];
-  m[12] = d[12] + d[15]; m[13] = d[13] + d[14]; m[14] = d[13] - d[14]; m[15] = d[12] - d[15];
-  d[0] = m[0] + m[1];  d[1] = m[0] - m[1];  d[2] = m[2] + m[3];  d[3] = m[3] - m[2];
-  d[4] = m[4] + m[5];  d[5] = m[4] - m[5];  d[6] = m[6] + m[7];  d[7] = m[7] - m[6];
-  d[8] = m[8] + m[9];  d[9] = m[8] - m[9];  d[10] = m[10] + m[11]; d[11] = m[11] - m[10];
-  d[12] = m[12] + m[13]; d[13] = m[12] - m[13]; d[14] = m[14] + m[15]; d[15] = m[15] - m[14];
-  int sa = 0;
-#pragma unroll
-  for (int k = 1; k < 16; k++) sa += abs(d[k]);
-  sa += abs(d[0]) >> 2;
-  return (sa + 1) >> 1;
+  return satd_4x4(O, P);
 }
 
 // Extended prediction row of a sub-block: columns -1..4 as the packed pairs
