@@ -61,6 +61,8 @@ def main():
         tot = v.sum()
         out[name] = {p: round(float(x / tot), 4) if tot else 0.0 for p, x in zip(PHASES, v)}
         out[name]["wave_clock_total"] = float(tot)
+        slot, life = float(buf[8 * k + 6]), float(buf[8 * k + 7])
+        out[name]["simd_slot_use"] = round(life / slot, 4) if slot else 0.0
     print(json.dumps({"config": args.config, "steps": args.steps, "phases": out}, indent=1))
     eng.close()
 

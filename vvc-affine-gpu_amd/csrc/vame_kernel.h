@@ -113,13 +113,31 @@ struct KParams {
 enum { kPhStage, kPhPredict, kPhCost, kPhGradient, kPhSolve, kPhTail, kNumPhases };
 #if VAME_PHASE_TIMING
 __device__ unsigned long long g_phase_cycles[2][8];  // [kernel: quad, ctu][phase]
-#define PH_DECL unsigned long long ph_acc[kNumPhases] = {}; unsigned long long ph_t = __builtin_amdgcn_s_memtime();
+#define PH_DECL unsigned long long ph_acc[kNumPhases] = {}; unsigned long long ph_t = __builtin_amdgcn_s_memtime(); const unsigned long long ph_t0 = ph_t;
 #define PH_MARK(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_acc[i] += t_ - ph_t; ph_t = t_; }
-#define PH_FLUSH { if (lane == 0) for (int i_ = 0; i_ < kNumPhases; i_++) atomicAdd(&g_phase_cycles[REGION == 128][i_], ph_acc[i_]); }
+// plus SIMD-slot use: [6] = waves x block lifetime, [7] = sum of wave lifetimes
+__shared__ unsigned long long s_ph_blk[3];  // min start, max end, sum of lifetimes
+__shared__ int s_ph_done;
+#define PH_FLUSH { \
+  if (lane == 0) { \
+    for (int i_ = 0; i_ < kNumPhases; i_++) atomicAdd(&g_phase_cycles[REGION == 128][i_], ph_acc[i_]); \
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
+    atomicMax(&s_ph_blk[1], t1_); \
+    atomicAdd(&s_ph_blk[2], t1_ - ph_t0); \
+    const int nw_ = (int)(blockDim.x >> 6); \
+    if (atomicAdd(&s_ph_done, 1) == nw_ - 1) { \
+      atomicAdd(&g_phase_cycles[REGION == 128][6], (unsigned long long)nw_ * (s_ph_blk[1] - s_ph_blk[0])); \
+      atomicAdd(&g_phase_cycles[REGION == 128][7], s_ph_blk[2]); \
+    } \
+  } }
+#define PH_INIT { if (tid == 0) { s_ph_blk[0] = ~0ull; s_ph_blk[1] = 0; s_ph_blk[2] = 0; s_ph_done = 0; } }
+#define PH_START { if (lane == 0) atomicMin(&s_ph_blk[0], ph_t0); }
 #else
 #define PH_DECL
 #define PH_MARK(i)
 #define PH_FLUSH
+#define PH_INIT
+#define PH_START
 #endif
 
 // ------------------------------------------------------------------ helpers
@@ -999,7 +1017,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     s_hdr[3] = it->ry;
   }
   for (int i = tid; i < kMaxCu * kNumMom; i += C::THREADS) (&s_val[0][0])[i] = 0;
+  PH_INIT
   __syncthreads();
+  PH_START
   const int hdr = __builtin_amdgcn_readfirstlane(s_hdr[0]);
   const int nCu = hdr & 0xFF, nWaves = (hdr >> 16) & 0xFF;
   const bool coop = ((hdr >> 8) & 0xFF) != 0;
