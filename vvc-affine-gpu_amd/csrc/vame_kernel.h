@@ -694,11 +694,15 @@ __device__ __forceinline__ void seg_solve(long long* V, double* M, int li, int L
 }
 
 // Per-CU refinement state.  `live` drops to 0 when the CU is out of frame or
-// when an update leaves its CPMVs unchanged: every later iteration would then
-// repeat the same prediction and cost (never strictly better) and the same
-// zero update, so skipping them leaves the result bit-identical.
-struct CuState {  // 64 bytes
+// when an update leaves its CPMVs unchanged -- or returns them to the previous
+// iteration's: the next CPMVs are a function of the current ones alone (the
+// prediction, gradients and solve depend on nothing else), so the iterations
+// after a fixed point or a period-2 cycle only repeat predictions and costs
+// already seen (never strictly better) -- skipping them leaves the result
+// bit-identical.
+struct CuState {
   int32_t cur[6];
+  int32_t prev[6];  // the CPMVs of the previous iteration (period-2 cycle test)
   int32_t best[6];
   int64_t bestCost;
   int32_t satd;
@@ -1142,6 +1146,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       }
       for (int i = 0; i < 6; i++) {
         st.cur[i] = c[i];
+        st.prev[i] = (int)0x80000000;  // outside the clamped CPMV range: never matches
         st.best[i] = c[i];
       }
       st.bestCost = kCostInit;
@@ -1289,13 +1294,15 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           clip_mv(c6[0], c6[1], cx, cy, W, H);
           clip_mv(c6[2], c6[3], cx, cy, W, H);
           clip_mv(c6[4], c6[5], cx, cy, W, H);
-          bool moved = false;
+          bool moved = false, back = true;
 #pragma unroll
           for (int i = 0; i < 6; i++) {
             moved |= c6[i] != st.cur[i];
+            back &= c6[i] == st.prev[i];
+            st.prev[i] = st.cur[i];
             st.cur[i] = c6[i];
           }
-          st.live = moved;
+          st.live = moved && !back;
         }
       }
       phase_sync(coop);
