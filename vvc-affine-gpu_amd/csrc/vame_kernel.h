@@ -308,14 +308,33 @@ __device__ __forceinline__ void hrow(const unsigned (&D)[5], const uint4& KA, co
   t[2] = dot2(D[1], KA.x, dot2(D[2], KA.y, dot2(D[3], KA.z, dot2(D[4], KA.w, -32768)))) >> 2;
   t[3] = dot2(D[1], KB.x, dot2(D[2], KB.y, dot2(D[3], KB.z, dot2(D[4], KB.w, -32768)))) >> 2;
 }
+// The same row before the >> 2 (the shift happens while packing, pack_shr2).
+__device__ __forceinline__ void hrow_raw(const unsigned (&D)[5], const uint4& KA, const uint4& KB,
+                                         int (&t)[4]) {
+  t[0] = dot2(D[0], KA.x, dot2(D[1], KA.y, dot2(D[2], KA.z, dot2(D[3], KA.w, -32768))));
+  t[1] = dot2(D[0], KB.x, dot2(D[1], KB.y, dot2(D[2], KB.z, dot2(D[3], KB.w, -32768))));
+  t[2] = dot2(D[1], KA.x, dot2(D[2], KA.y, dot2(D[3], KA.z, dot2(D[4], KA.w, -32768))));
+  t[3] = dot2(D[1], KB.x, dot2(D[2], KB.y, dot2(D[3], KB.z, dot2(D[4], KB.w, -32768))));
+}
+// (lo >> 2) | (hi >> 2) << 16 in two instructions: the second shift writes its
+// low 16 bits straight into the upper half (SDWA dst_sel:WORD_1, preserve).
+__device__ __forceinline__ unsigned pack_shr2(int lo, int hi) {
+  unsigned d = (unsigned)(lo >> 2);
+  asm("v_ashrrev_i32_sdwa %0, 2, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "
+      "src1_sel:DWORD"
+      : "+v"(d)
+      : "v"(hi));
+  return d;
+}
 // Vertical pass, streamed: row pair k = (t[2k], t[2k+1]) (pair 4 = (t[8], 0))
 // feeds output row r through tap-pair set G_{r&1}, entry k - (r >> 1)
 // (aux_functions.cl:1182-1223); integer sums, so the order is free.
+// t0/t1 are the raw horizontal sums (before >> 2).
 __device__ __forceinline__ void vpair(int k, const int (&t0)[4], const int (&t1)[4],
                                       const uint4& G0, const uint4& G1, int (&acc)[4][4]) {
 #pragma unroll
   for (int c = 0; c < 4; c++) {
-    const unsigned P = pack16(t0[c], t1[c]);
+    const unsigned P = pack_shr2(t0[c], t1[c]);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int m = k - (r >> 1);
@@ -349,8 +368,8 @@ __device__ __forceinline__ void filter_rows(const unsigned* src, const uint4& KA
         }
     }
     int t0[4], t1[4] = {0, 0, 0, 0};
-    hrow(D[cb][0], KA, KB, t0);
-    if (k < 4) hrow(D[cb][1], KA, KB, t1);
+    hrow_raw(D[cb][0], KA, KB, t0);
+    if (k < 4) hrow_raw(D[cb][1], KA, KB, t1);
     vpair(k, t0, t1, G0, G1, acc);
     __builtin_amdgcn_sched_barrier(0);
   }
