@@ -208,11 +208,14 @@ __device__ __forceinline__ int affine_bits(const int* c, int ncp) {
   return b;
 }
 
-__device__ __forceinline__ int cvt_i32_f64(double d) {  // v_cvt_i32_f64 semantics
-  if (d != d) return 0;
-  if (d >= 2147483647.0) return 2147483647;
-  if (d <= -2147483648.0) return (int)0x80000000u;
-  return (int)d;
+// (int)double with the semantics the reference's kernels get from the GPU:
+// truncation, NaN -> 0, out-of-range values saturate -- exactly what
+// v_cvt_i32_f64 does, so it is issued directly (a C++ cast of an out-of-range
+// value is undefined and would need explicit checks).
+__device__ __forceinline__ int cvt_i32_f64(double d) {
+  int r;
+  asm("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(d));
+  return r;
 }
 
 // aux_functions.cl:2194-2215
