@@ -590,29 +590,6 @@ __device__ __forceinline__ void grad_sb(int sx, int sy, const Geo& g, const uint
   S[0] = sxx; S[1] = sxy; S[2] = syy; S[3] = sxe; S[4] = sye;
 }
 
-// Element (r, c) of a CU's normal equations (affine.cl:759-763) from its
-// reduced values V; column N is the right-hand side (<< 3, affine.cl:705).
-// Integer sums below 2^53 convert to double exactly.
-template <int NCP>
-__device__ __forceinline__ long long reduced_value(const long long* V, int i, bool coop);
-
-template <int NCP>
-__device__ __forceinline__ double eq_element(const long long* V, int r, int c, bool coop) {
-  if constexpr (NCP == 2) {
-    if (c == 4) return (double)(reduced_value<2>(V, 10 + r, coop) * 8);
-    const int lo = min(r, c), hi = max(r, c);  // symmetric: A00 A01 A02 A03 A11 A12 A13 A22 A23 A33
-    return (double)reduced_value<2>(V, lo == 0 ? hi : lo == 1 ? 3 + hi : lo == 2 ? 5 + hi : 9, coop);
-  } else {
-    // regressor r = (gradient t: 0 x / 1 y, monomial m: 0 1 / 1 u / 2 v):
-    // gx, u gx, gy, u gy, v gx, v gy (affine.cl:684-689)
-    const int tr = (r == 2 || r == 3 || r == 5) ? 1 : 0, mr = (r == 1 || r == 3) ? 1 : (r >= 4 ? 2 : 0);
-    if (c == 6) return (double)(reduced_value<3>(V, 18 + 3 * tr + mr, coop) * 8);
-    const int tc = (c == 2 || c == 3 || c == 5) ? 1 : 0, mc = (c == 1 || c == 3) ? 1 : (c >= 4 ? 2 : 0);
-    const int prod = mr == 0 ? mc : mc == 0 ? mr : (mr == 1 && mc == 1) ? 3 : (mr == 2 && mc == 2) ? 5 : 4;
-    return (double)reduced_value<3>(V, 6 * (tr + tc) + prod, coop);
-  }
-}
-
 // VTM solveEqual (affine.cl:782-856), forward elimination shared by the lanes
 // of a CU's segment (li = lane in the segment, Ls = segment size) on the CU's
 // matrix M (row r = private_dEqualCoeff[r + 1], N + 1 columns) in LDS:
@@ -700,14 +677,55 @@ __device__ __forceinline__ void back_substitute(const double* M, int lw, int lh,
   }
 }
 
+// Which reduced value feeds matrix element e = r * (N + 1) + c (eq_element's
+// mapping as a table): bits 0-6 the value index, bit 7 set on the right-hand
+// side column (scaled by 8).  2 CP: elements 0..19, 3 CP: 32..73.
+struct EqMap {
+  uint8_t v[80];
+};
+constexpr uint8_t eq_map_entry(int ncp, int r, int c) {
+  if (ncp == 2) {
+    if (c == 4) return (uint8_t)(0x80 | (10 + r));
+    const int lo = r < c ? r : c, hi = r < c ? c : r;
+    return (uint8_t)(lo == 0 ? hi : lo == 1 ? 3 + hi : lo == 2 ? 5 + hi : 9);
+  }
+  const int tr = (r == 2 || r == 3 || r == 5) ? 1 : 0, mr = (r == 1 || r == 3) ? 1 : (r >= 4 ? 2 : 0);
+  if (c == 6) return (uint8_t)(0x80 | (18 + 3 * tr + mr));
+  const int tc = (c == 2 || c == 3 || c == 5) ? 1 : 0, mc = (c == 1 || c == 3) ? 1 : (c >= 4 ? 2 : 0);
+  const int prod = mr == 0 ? mc : mc == 0 ? mr : (mr == 1 && mc == 1) ? 3 : (mr == 2 && mc == 2) ? 5 : 4;
+  return (uint8_t)(6 * (tr + tc) + prod);
+}
+constexpr EqMap make_eq_map() {
+  EqMap m{};
+  for (int e = 0; e < 20; e++) m.v[e] = eq_map_entry(2, e / 5, e % 5);
+  for (int e = 0; e < 42; e++) m.v[32 + e] = eq_map_entry(3, e / 7, e % 7);
+  return m;
+}
+__constant__ EqMap kEqMap = make_eq_map();
+
 // Build, eliminate and back-substitute one CU's system with its segment; the
-// segment's first lane returns the deltas.
+// segment's first lane returns the deltas.  The integer sums convert exactly
+// (|value| < 2^53): autonomous items hold them as int32 halves, value =
+// hi * 2^24 + lo, formed in double as fma(hi, 2^24, lo) (both terms exact, the
+// sum exact); the right-hand side is scaled by 8 exactly.
 template <int NCP>
-__device__ __forceinline__ void seg_solve(long long* V, double* M, int li, int Ls, bool act,
-                                          bool coop, int lw, int lh, double dd[6]) {
-  constexpr int N = 2 * NCP, NC = N + 1;
+__device__ __forceinline__ void seg_solve(long long* V, double* M, const uint8_t* eqmap, int li,
+                                          int Ls, bool act, bool coop, int lw, int lh,
+                                          double dd[6]) {
+  constexpr int N = 2 * NCP, NC = N + 1, NV = NCP == 2 ? kNumVal2 : kNumMom;
   if (act) {
-    for (int e = li; e < N * NC; e += Ls) M[e] = eq_element<NCP>(V, e / NC, e % NC, coop);
+    const int* V32 = reinterpret_cast<const int*>(V);
+    for (int e = li; e < N * NC; e += Ls) {
+      const int m = eqmap[(NCP == 2 ? 0 : 32) + e];
+      const int vi = m & 0x7F;
+      const double sc = (m & 0x80) ? 8.0 : 1.0;
+      double x;
+      if (coop)
+        x = (double)V[vi];
+      else
+        x = fma((double)V32[NV + vi], 16777216.0, (double)(unsigned)V32[vi]);
+      M[e] = x * sc;
+    }
     if (coop && li < kNumMom) V[li] = 0;  // cooperative items accumulate with atomics
   }
   wave_sync();
@@ -989,15 +1007,6 @@ __device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v
   }
 }
 
-// Reduced value i of a CU: int64 (cooperative items) or int32 halves
-// (autonomous items, see reduce_equations_c).
-template <int NCP>
-__device__ __forceinline__ long long reduced_value(const long long* V, int i, bool coop) {
-  constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
-  if (coop) return V[i];
-  const int* V32 = reinterpret_cast<const int*>(V);
-  return (long long)V32[NV + i] * (1ll << 24) + (long long)(unsigned)V32[i];
-}
 
 template <int REGION>
 __device__ __forceinline__ void affine_me_body(const KParams& p) {
@@ -1009,6 +1018,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   __shared__ __attribute__((aligned(16))) long long s_val[kMaxCu][kNumMom];
   __shared__ double s_mat[kMaxCu][42];  // per CU: N x (N + 1) system, N <= 6
   __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
+  __shared__ uint8_t s_eqmap[80];
   __shared__ CuState s_st[kMaxCu];
   __shared__ CuSlot s_cu[kMaxCu];
   __shared__ WaveDesc s_wave[kMaxWaves];
@@ -1037,6 +1047,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   if (tid < kMaxCu) s_cu[tid] = it->cu[tid];
   if (tid < kMaxWaves) s_wave[tid] = it->wave[tid];
   if (tid < 48) s_coef[tid] = reinterpret_cast<const uint4*>(&kCoefTab)[tid];
+  if (tid < 80) s_eqmap[tid] = kEqMap.v[tid];
   if (tid == 0) {
     s_hdr[0] = it->nCu | (it->coop << 8) | (it->nWaves << 16) | (it->logL << 24);
     s_hdr[2] = it->rx;
@@ -1297,9 +1308,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         double* M = s_mat[cuS < 0 ? 0 : cuS];
         const CuSlot cs = s_cu[cuS < 0 ? 0 : cuS];
         if (ncp == 3)
-          seg_solve<3>(V, M, loc, Ls, act, coop, cs.lw, cs.lh, dd);
+          seg_solve<3>(V, M, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd);
         else
-          seg_solve<2>(V, M, loc, Ls, act, coop, cs.lw, cs.lh, dd);
+          seg_solve<2>(V, M, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd);
         if (act && loc == 0) {
           CuState& st = s_st[cuS];
           // affine.cl:884-893 (scaleDeltaMvs order: LT=(d0,d2), RT=(d1,d3), LB=(d4,d5))
