@@ -1239,23 +1239,41 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       PH_MARK(kPhPredict)
 
       // =============== cost, best update (affine.cl:416-457) ===============
+      // The rate (calc_affine_bits, aux_functions.cl:2140-2189) is spread over
+      // the CU's first lanes: lane j < 2 * nCP codes component j of the MVD
+      // against the zero predictor, three DPP steps sum them into the CU's
+      // lane 7, which forms the cost and keeps the strict best.
       const bool lastIter = iter == niter;
-      if (lane < nCuW) {
-        const int k = cuB + lane;
-        CuState& st = s_st[k];
-        if (iter == 0 || st.live) {
-          const int bits = affine_bits(st.cur, ncp) + kRuiBits;
-          const float prod = __fmul_rn(p.lambda, (float)bits);
-          const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
-          if (cost < st.bestCost) {
-            st.bestCost = cost;
-            for (int i = 0; i < 6; i++) st.best[i] = st.cur[i];
-          }
+      {
+        int b = 0;
+        const CuState& sr = s_st[myCu < 0 ? 0 : myCu];
+        const bool rate = myCu >= 0 && (iter == 0 || sr.live);
+        if (rate && local < 2 * ncp) {
+          int v = to_quarter(sr.cur[local]);
+          if (local >= 2) v -= to_quarter(sr.cur[local & 1]);
+          b = eg_bits(v);
         }
-        st.satd = 0;
+        b += dpp32<0x111, 0xF>(b);  // row_shr:1, 2, 4: lane 7 of the CU sums lanes 0..7
+        b += dpp32<0x112, 0xF>(b);
+        b += dpp32<0x114, 0xF>(b);
+        if (myCu >= 0 && local == 7) {
+          CuState& st = s_st[myCu];
+          if (rate) {
+            const float prod = __fmul_rn(p.lambda, (float)(b + kRuiBits));
+            const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
+            if (cost < st.bestCost) {
+              st.bestCost = cost;
+              for (int i = 0; i < 6; i++) st.best[i] = st.cur[i];
+            }
+          }
+          st.satd = 0;
+        }
       }
       PH_MARK(kPhCost)
-      if (lastIter) break;  // uniform
+      if (lastIter) {  // uniform; the results below are written by other lanes
+        phase_sync(coop);
+        break;
+      }
 
       // =============== gradients + normal equations (affine.cl:477-752) ===============
       {
