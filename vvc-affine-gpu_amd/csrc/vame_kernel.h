@@ -624,10 +624,17 @@ __device__ __forceinline__ void seg_eliminate(double* M, int li, int Ls, bool ac
     wave_sync();
     const int cols = N + 1 - i, E = (N - i) * cols;  // constants after unrolling
     if (act) {
-      for (int e = li; e < E; e += Ls) {
-        const int r = i + e / cols, k = i + e % cols;
-        M[r * NC + k] = __dsub_rn(M[r * NC + k], __ddiv_rn(__dmul_rn(M[(i - 1) * NC + k], M[r * NC + i - 1]),
-                                                           M[(i - 1) * NC + i - 1]));
+      // at most two elements per lane (E <= 30, Ls >= 16); e / cols for e < 64
+      // by a multiply-shift (exact for these small operands)
+      constexpr int kMagic[7] = {0, 0, 513, 342, 257, 206, 171};  // ceil(1024 / cols)
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int e = li + q * Ls;
+        if (e < E) {
+          const int dr = (e * kMagic[N + 1 - i]) >> 10, r = i + dr, k = i + e - dr * cols;
+          M[r * NC + k] = __dsub_rn(M[r * NC + k], __ddiv_rn(__dmul_rn(M[(i - 1) * NC + k], M[r * NC + i - 1]),
+                                                             M[(i - 1) * NC + i - 1]));
+        }
       }
     }
     wave_sync();
