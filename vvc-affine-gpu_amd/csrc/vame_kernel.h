@@ -969,14 +969,24 @@ __device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int
                                                    long long* dst) {
   constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
   constexpr int K = 2 * NV;
+  // the first halving step pairs x[j] = lo(value j) with x[j + NV] = hi(value
+  // j): fused with producing the value, so only NV halves are ever live
+  constexpr int B0 = Schedule<LOGS, K>::bit(0);
   int x[K];
 #pragma unroll
   for (int i = 0; i < NV; i++) {
     const long long e = eq_value<NCP>(i, S, u, v);
-    x[i] = (int)((unsigned)e & 0xFFFFFFu);
-    x[NV + i] = (int)(e >> 24);
+    const int lo = (int)((unsigned)e & 0xFFFFFFu), hi = (int)(e >> 24);
+    if constexpr (B0 >= 4) {
+      const auto r = B0 == 5 ? __builtin_amdgcn_permlane32_swap((unsigned)lo, (unsigned)hi, false, false)
+                             : __builtin_amdgcn_permlane16_swap((unsigned)lo, (unsigned)hi, false, false);
+      x[i] = (int)(r[0] + r[1]);
+    } else {
+      const bool beta = lane_bit(B0);
+      x[i] = xchg_dpp<B0>(beta ? hi : lo, beta ? lo : hi);
+    }
   }
-  butterfly<LOGS, 0, K>(x);
+  butterfly<LOGS, 1, NV>(x);
   constexpr int CNT = Final<LOGS, K>::count();
   const int lidx = __lane_id() & ((1 << LOGS) - 1);
   int off, limit;
