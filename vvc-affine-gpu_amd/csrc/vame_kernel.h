@@ -311,13 +311,29 @@ __device__ __forceinline__ void hrow(const unsigned (&D)[5], const uint4& KA, co
   t[2] = dot2(D[1], KA.x, dot2(D[2], KA.y, dot2(D[3], KA.z, dot2(D[4], KA.w, -32768)))) >> 2;
   t[3] = dot2(D[1], KB.x, dot2(D[2], KB.y, dot2(D[3], KB.z, dot2(D[4], KB.w, -32768)))) >> 2;
 }
-// The same row before the >> 2 (the shift happens while packing, pack_shr2).
+// The same row before the >> 2 (the shift happens while packing, pack_shr2),
+// with the offsets re-based so that no accumulator needs a non-inline
+// constant: the six taps of every phase sum to 64, so
+//   sum_v f_v * ((S_v - 32768) >> 2) + 512 + (8192 << 6)
+//     = sum_v f_v * ((S_v - 32768) >> 2 + 8192 + 8)
+//     = sum_v f_v * ((S_v + 32) >> 2)
+// (32768 is a multiple of 4, so the floor shifts by exactly 8192): the rows
+// start from +32 and the vertical accumulators from 0.  (S_v + 32) >> 2 stays
+// within [-5619, 22008], so the packed int16 pairs are exact.
+// a.lo*b.lo + a.hi*b.hi + K for an inline constant K, as the VOP3 form (the
+// compiler picks the accumulate-in-place v_dot2c form and a v_mov of K)
+template <int K>
+__device__ __forceinline__ int dot2k(unsigned a, unsigned b) {
+  int r;
+  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "i"(K));
+  return r;
+}
 __device__ __forceinline__ void hrow_raw(const unsigned (&D)[5], const uint4& KA, const uint4& KB,
                                          int (&t)[4]) {
-  t[0] = dot2(D[0], KA.x, dot2(D[1], KA.y, dot2(D[2], KA.z, dot2(D[3], KA.w, -32768))));
-  t[1] = dot2(D[0], KB.x, dot2(D[1], KB.y, dot2(D[2], KB.z, dot2(D[3], KB.w, -32768))));
-  t[2] = dot2(D[1], KA.x, dot2(D[2], KA.y, dot2(D[3], KA.z, dot2(D[4], KA.w, -32768))));
-  t[3] = dot2(D[1], KB.x, dot2(D[2], KB.y, dot2(D[3], KB.z, dot2(D[4], KB.w, -32768))));
+  t[0] = dot2(D[0], KA.x, dot2(D[1], KA.y, dot2(D[2], KA.z, dot2k<32>(D[3], KA.w))));
+  t[1] = dot2(D[0], KB.x, dot2(D[1], KB.y, dot2(D[2], KB.z, dot2k<32>(D[3], KB.w))));
+  t[2] = dot2(D[1], KA.x, dot2(D[2], KA.y, dot2(D[3], KA.z, dot2k<32>(D[4], KA.w))));
+  t[3] = dot2(D[1], KB.x, dot2(D[2], KB.y, dot2(D[3], KB.z, dot2k<32>(D[4], KB.w))));
 }
 // (lo >> 2) | (hi >> 2) << 16 in two instructions: the second shift writes its
 // low 16 bits straight into the upper half (SDWA dst_sel:WORD_1, preserve).
@@ -344,7 +360,7 @@ __device__ __forceinline__ void vpair(int k, const int (&t0)[4], const int (&t1)
       if (m < 0 || m > 3 || ((r & 1) == 0 && m == 3)) continue;  // set 0 ends with (0,0)
       const uint4& G = (r & 1) ? G1 : G0;
       const unsigned g = m == 0 ? G.x : m == 1 ? G.y : m == 2 ? G.z : G.w;
-      acc[r][c] = dot2(P, g, acc[r][c]);
+      acc[r][c] = m == 0 ? dot2k<0>(P, g) : dot2(P, g, acc[r][c]);  // first tap pair starts the sum
     }
   }
 }
@@ -484,14 +500,19 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   const uint4 KA = s_coef[fx * 3 + sp], KB = s_coef[fx * 3 + sp + 1];
   const uint4 G0 = s_coef[fy * 3 + 0], G1 = s_coef[fy * 3 + 1];
   int acc[4][4];
-#pragma unroll
-  for (int r = 0; r < 4; r++)
-#pragma unroll
-    for (int c = 0; c < 4; c++) acc[r][c] = 524800;  // (1 << 9) + (8192 << 6)
   if (inTile) {
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) acc[r][c] = 0;  // offsets folded into the rows (hrow_raw);
+                                                  // the first tap pair overwrites it (vpair)
     const unsigned* src = reinterpret_cast<const unsigned*>(s_tile) + ((ty * TP + tx) >> 1);
     filter_rows<TP / 2>(src, KA, KB, G0, G1, acc);
   } else {
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) acc[r][c] = 524800;  // (1 << 9) + (8192 << 6)
     filter_rows_global(ref, wx, wy, W, H, KA, KB, reinterpret_cast<const unsigned*>(s_coef), fy,
                        acc);
   }
