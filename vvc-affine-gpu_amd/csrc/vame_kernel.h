@@ -1229,10 +1229,12 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 
     for (int iter = 0; iter <= niter; iter++) {
       // =============== prediction + SATD (affine.cl:208-393) ===============
-      int satdLane = 0;
+      // Everything a lane produces here is only read while its CU is live
+      // (the CU's lanes are uniformly live or not), so the whole step runs
+      // under `live`: the DPP neighbour reads at the CU's edges may see lanes
+      // of other CUs, whose columns the border replication discards.
       uint2 Pr[4], Og[4];  // this lane's prediction and original rows (packed pairs)
-#pragma unroll
-      for (int r = 0; r < 4; r++) Pr[r] = Og[r] = make_uint2(0, 0);
+      uint4 X[6];          // extended rows 0..3 (X[1..4]) and the neighbours' edges
       const bool live = active && s_st[myCu < 0 ? 0 : myCu].live;
       if (live && !(VAME_ABLATE & 8)) {
         Geo gp = g;
@@ -1241,8 +1243,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         int cp[6];
         for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
         const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
-        satdLane = predict_sb<C::TILE, C::TP>(f, sxp, syp, gp, s_tile, tx0, ty0, ref, cur, W, H,
-                                              s_coef, Pr, Og);
+        const int satdLane = predict_sb<C::TILE, C::TP>(f, sxp, syp, gp, s_tile, tx0, ty0, ref, cur,
+                                                        W, H, s_coef, Pr, Og);
         if (VAME_DUP & 1) {
           MvField f2 = f;
           opaque(f2.bx);
@@ -1252,18 +1254,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           s2 += (int)(P2[0].x ^ P2[3].y ^ O2[1].x);
           asm volatile("" ::"v"(s2));
         }
-      }
-      // extended rows (neighbour columns by DPP), edge rows published for the
-      // sub-blocks above and below
-      uint4 X[6];
+        // extended rows (neighbour columns by DPP), edge rows published for
+        // the sub-blocks above and below
 #pragma unroll
-      for (int r = 0; r < 4; r++)
-        X[r + 1] = ext_row(Pr[r], dpp32<0x138, 0xF>((int)Pr[r].y), dpp32<0x130, 0xF>((int)Pr[r].x));
-      if (myCu >= 0) {
+        for (int r = 0; r < 4; r++)
+          X[r + 1] = ext_row(Pr[r], dpp32<0x138, 0xF>((int)Pr[r].y), dpp32<0x130, 0xF>((int)Pr[r].x));
         s_top[sbIdx] = X[1];
         s_bot[sbIdx] = X[4];
-      }
-      {
         const int v = logS == 4 ? seg_sum_c<4>(satdLane)
                       : logS == 5 ? seg_sum_c<5>(satdLane) : seg_sum_c<6>(satdLane);
         if (leader) {
