@@ -100,7 +100,8 @@ struct KParams {
 #endif
 // VAME_DUP (timing-only builds, results stay correct): run a phase twice to
 // price it in throughput terms: bit 0 prediction, bit 1 gradient, bit 2
-// equation reduction, bit 3 tile staging.
+// equation reduction, bit 3 tile staging, bit 4 the solve (on a copy of the
+// system).
 #ifndef VAME_DUP
 #define VAME_DUP 0
 #endif
@@ -736,7 +737,7 @@ __constant__ EqMap kEqMap = make_eq_map();
 // (|value| < 2^53): autonomous items hold them as int32 halves, value =
 // hi * 2^24 + lo, formed in double as fma(hi, 2^24, lo) (both terms exact, the
 // sum exact); the right-hand side is scaled by 8 exactly.
-template <int NCP>
+template <int NCP, bool KEEP_V = false>
 __device__ __forceinline__ void seg_solve(long long* V, double* M, const uint8_t* eqmap, int li,
                                           int Ls, bool act, bool coop, int lw, int lh,
                                           double dd[6]) {
@@ -754,11 +755,17 @@ __device__ __forceinline__ void seg_solve(long long* V, double* M, const uint8_t
         x = fma((double)V32[NV + vi], 16777216.0, (double)(unsigned)V32[vi]);
       M[e] = x * sc;
     }
-    if (coop && li < kNumMom) V[li] = 0;  // cooperative items accumulate with atomics
+    if (!KEEP_V && coop && li < kNumMom) V[li] = 0;  // cooperative items accumulate with atomics
   }
   wave_sync();
   seg_eliminate<N>(M, li, Ls, act);
-  if (act && li == 0) back_substitute<NCP>(M, lw, lh, dd);
+  if (act && li == 0) {
+    back_substitute<NCP>(M, lw, lh, dd);
+    // the deltas for the CU's update lanes (M is dead now)
+#pragma unroll
+    for (int i = 0; i < 6; i++) M[i] = dd[i];
+  }
+  wave_sync();
 }
 
 // Per-CU refinement state.  `live` drops to 0 when the CU is out of frame or
@@ -1055,6 +1062,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   __shared__ uint4 s_bot[C::NSB];  // extended row 3
   __shared__ __attribute__((aligned(16))) long long s_val[kMaxCu][kNumMom];
   __shared__ double s_mat[kMaxCu][42];  // per CU: N x (N + 1) system, N <= 6
+  __shared__ double s_mat_dup[(VAME_DUP & 16) ? kMaxCu : 1][42];
   __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
   __shared__ uint8_t s_eqmap[80];
   __shared__ CuState s_st[kMaxCu];
@@ -1291,6 +1299,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         b += dpp32<0x111, 0xF>(b);  // row_shr:1, 2, 4: lane 7 of the CU sums lanes 0..7
         b += dpp32<0x112, 0xF>(b);
         b += dpp32<0x114, 0xF>(b);
+        int better = 0;
         if (myCu >= 0 && local == 7) {
           CuState& st = s_st[myCu];
           if (rate) {
@@ -1298,11 +1307,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
             if (cost < st.bestCost) {
               st.bestCost = cost;
-              for (int i = 0; i < 6; i++) st.best[i] = st.cur[i];
+              better = 1;
             }
           }
           st.satd = 0;
         }
+        better = __builtin_amdgcn_update_dpp(0, better, 0x157, 0xF, 0xF, false);  // row_newbcast:7
+        if (myCu >= 0 && local < 6 && better) s_st[myCu].best[local] = s_st[myCu].cur[local];
       }
       PH_MARK(kPhCost)
       if (lastIter) {  // uniform; the results below are written by other lanes
@@ -1360,43 +1371,59 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         long long* V = s_val[cuS < 0 ? 0 : cuS];
         double* M = s_mat[cuS < 0 ? 0 : cuS];
         const CuSlot cs = s_cu[cuS < 0 ? 0 : cuS];
+        if constexpr ((VAME_DUP & 16) != 0) {  // timing-only: a throw-away solve first
+          double dd2[6] = {0, 0, 0, 0, 0, 0};
+          double* M2 = s_mat_dup[cuS < 0 ? 0 : cuS];
+          if (ncp == 3)
+            seg_solve<3, true>(V, M2, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd2);
+          else
+            seg_solve<2, true>(V, M2, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd2);
+          asm volatile("" ::"v"(dd2[0]), "v"(dd2[1]), "v"(dd2[3]));
+          wave_sync();
+        }
         if (ncp == 3)
           seg_solve<3>(V, M, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd);
         else
           seg_solve<2>(V, M, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd);
-        if (act && loc == 0) {
+        // affine.cl:860-893, one CPMV component per lane: lane j < 6 of the
+        // CU applies scaleDeltaMvs to its delta (LT=(d0,d2), RT=(d1,d3),
+        // LB=(d4,d5)), clampCpmvs and clipCpmvs, and the CU's lane 7 sums
+        // the moved / cycle flags (DPP) into the CU's `live`
+        bool liveNew = false;
+        if (act && loc < 8) {
           CuState& st = s_st[cuS];
-          // affine.cl:884-893 (scaleDeltaMvs order: LT=(d0,d2), RT=(d1,d3), LB=(d4,d5))
-          int c6[6];
-          c6[0] = (int)((unsigned)st.cur[0] + (unsigned)scale_delta(dd[0]));
-          c6[1] = (int)((unsigned)st.cur[1] + (unsigned)scale_delta(dd[2]));
-          c6[2] = (int)((unsigned)st.cur[2] + (unsigned)scale_delta(dd[1]));
-          c6[3] = (int)((unsigned)st.cur[3] + (unsigned)scale_delta(dd[3]));
-          c6[4] = (int)((unsigned)st.cur[4] + (unsigned)scale_delta(dd[4]));
-          c6[5] = (int)((unsigned)st.cur[5] + (unsigned)scale_delta(dd[5]));
-          const int cx = ctuX + cs.x, cy = ctuY + cs.y;
-#pragma unroll
-          for (int i = 0; i < 6; i++) c6[i] = clampi(c6[i], kMvMin, kMvMax);
-          clip_mv(c6[0], c6[1], cx, cy, W, H);
-          clip_mv(c6[2], c6[3], cx, cy, W, H);
-          clip_mv(c6[4], c6[5], cx, cy, W, H);
-          bool moved = false, back = true;
-#pragma unroll
-          for (int i = 0; i < 6; i++) {
-            moved |= c6[i] != st.cur[i];
-            back &= c6[i] == st.prev[i];
-            st.prev[i] = st.cur[i];
-            st.cur[i] = c6[i];
+          int f = 0;
+          if (loc < 6) {
+            const int j = loc;
+            const double d = M[j == 1 ? 2 : j == 2 ? 1 : j];
+            const int cj = st.cur[j], pj = st.prev[j];
+            int v = (int)((unsigned)cj + (unsigned)scale_delta(d));
+            v = clampi(v, kMvMin, kMvMax);
+            const int pos = (j & 1) ? ctuY + cs.y : ctuX + cs.x, lim = (j & 1) ? H : W;
+            v = clampi(v, shl(-128 - 8 - pos + 1, 4), shl(lim + 8 - pos - 1, 4));  // clipMv
+            f = (v != cj ? 1 : 0) | (v != pj ? 16 : 0);
+            st.prev[j] = cj;
+            st.cur[j] = v;
           }
-          st.live = moved && !back;
+          f += dpp32<0x111, 0xF>(f);  // row_shr:1, 2, 4: lane 7 sums lanes 0..7
+          f += dpp32<0x112, 0xF>(f);
+          f += dpp32<0x114, 0xF>(f);
+          if (loc == 7) {
+            liveNew = (f & 15) != 0 && (f >> 4) != 0;  // moved, and not back to the previous
+            st.live = liveNew;
+          }
+        }
+        if (!coop) {  // leave once every CU of this wave is settled (wave-local)
+          if (__ballot(liveNew) == 0) break;
         }
       }
       phase_sync(coop);
       PH_MARK(kPhSolve)
-      // leave once every CU of this wave (autonomous) / item (cooperative) is settled
-      bool anyLive = false;
-      for (int k = cuB; k < cuE; k++) anyLive |= s_st[k].live != 0;
-      if (!anyLive) break;  // uniform: same flags read by every lane after the sync
+      if (coop) {  // leave once every CU of the item is settled (flags read after the sync)
+        bool anyLive = false;
+        for (int k = cuB; k < cuE; k++) anyLive |= s_st[k].live != 0;
+        if (!anyLive) break;
+      }
     }
     // =============== results (affine.cl:928-957) ===============
     if (lane < nCuW) {
