@@ -755,7 +755,11 @@ __device__ __forceinline__ void seg_solve(long long* V, double* M, const uint8_t
         x = fma((double)V32[NV + vi], 16777216.0, (double)(unsigned)V32[vi]);
       M[e] = x * sc;
     }
-    if (!KEEP_V && coop && li < kNumMom) V[li] = 0;  // cooperative items accumulate with atomics
+    if (!KEEP_V && coop && li < kNumMom) {  // cooperative items accumulate with atomics
+      int z = 0;
+      opaque(z);  // a fresh zero, not a loop-carried (spilled) constant
+      reinterpret_cast<int2*>(V)[li] = make_int2(z, z);
+    }
   }
   wave_sync();
   seg_eliminate<N>(M, li, Ls, act);
@@ -763,7 +767,7 @@ __device__ __forceinline__ void seg_solve(long long* V, double* M, const uint8_t
     back_substitute<NCP>(M, lw, lh, dd);
     // the deltas for the CU's update lanes (M is dead now)
 #pragma unroll
-    for (int i = 0; i < 6; i++) M[i] = dd[i];
+    for (int i = 0; i < 2 * NCP; i++) M[i] = dd[i];
   }
   wave_sync();
 }
@@ -1196,7 +1200,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 
     // ---- per-CU initial CPMVs (2 CP: zero; 3 CP: derived from the 2-CP winner)
     if (lane < nCuW) {
-      const int k = cuB + lane;
+      int k = cuB + lane;
+      opaque(k);
       const CuSlot cs = s_cu[k];
       CuState& st = s_st[k];
       const int cx = ctuX + cs.x, cy = ctuY + cs.y;
@@ -1289,11 +1294,14 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       const bool lastIter = iter == niter;
       {
         int b = 0;
-        const CuState& sr = s_st[myCu < 0 ? 0 : myCu];
-        const bool rate = myCu >= 0 && (iter == 0 || sr.live);
-        if (rate && local < 2 * ncp) {
-          int v = to_quarter(sr.cur[local]);
-          if (local >= 2) v -= to_quarter(sr.cur[local & 1]);
+        int cuR = myCu, locR = local;  // recomputed addresses (no loop-carried copies)
+        opaque(cuR);
+        opaque(locR);
+        const CuState& sr = s_st[cuR < 0 ? 0 : cuR];
+        const bool rate = cuR >= 0 && (iter == 0 || sr.live);
+        if (rate && locR < 2 * ncp) {
+          int v = to_quarter(sr.cur[locR]);
+          if (locR >= 2) v -= to_quarter(sr.cur[locR & 1]);
           b = eg_bits(v);
         }
         b += dpp32<0x111, 0xF>(b);  // row_shr:1, 2, 4: lane 7 of the CU sums lanes 0..7
@@ -1340,7 +1348,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           }
         }
         if (!(VAME_ABLATE & 4)) {
-          long long* dst = s_val[myCu < 0 ? 0 : myCu];
+          int cuV = myCu;
+          opaque(cuV);
+          long long* dst = s_val[cuV < 0 ? 0 : cuV];
           if (ncp == 2)
             reduce_equations<2>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
           else
@@ -1393,7 +1403,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         if (act && loc < 8) {
           CuState& st = s_st[cuS];
           int f = 0;
-          if (loc < 6) {
+          if (loc < 2 * ncp) {  // 2 CP: LB stays (0, 0)
             const int j = loc;
             const double d = M[j == 1 ? 2 : j == 2 ? 1 : j];
             const int cj = st.cur[j], pj = st.prev[j];
@@ -1427,7 +1437,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     }
     // =============== results (affine.cl:928-957) ===============
     if (lane < nCuW) {
-      const int k = cuB + lane;
+      int k = cuB + lane;
+      opaque(k);
       const CuState& st = s_st[k];
       const CuSlot cs = s_cu[k];
       const int mode = cs.align * 2 + (ncp - 2);
