@@ -173,7 +173,7 @@ static int spread_over_limit(int a, int b, int c, int d) {
 
 /* aux_functions.cl:146-212 deriveMv{2,3}Cps_and_spread; then roundAndClipMv */
 static omv subblock_mv(const ocpmvs *cp, int nCP, int w, int h, int sx, int sy,
-                       int cux, int cuy, int W, int H) {
+                       int cux, int cuy, int W, int H, int *spread) {
   int lw = ilog2(w), lh = ilog2(h);
   int hx = shl(cp->RT.x - cp->LT.x, 7 - lw);
   int hy = shl(cp->RT.y - cp->LT.y, 7 - lw);
@@ -187,7 +187,8 @@ static omv subblock_mv(const ocpmvs *cp, int nCP, int w, int h, int sx, int sy,
   }
   int bx = shl(cp->LT.x, 7), by = shl(cp->LT.y, 7);
   int px, py;
-  if (spread_over_limit(hx, hy, vx, vy)) {
+  *spread = spread_over_limit(hx, hy, vx, vy);
+  if (*spread) {
     px = w >> 1;
     py = h >> 1;
   } else {
@@ -228,6 +229,94 @@ static void predict_4x4(const uint16_t *ref, int W, int H, int x0, int y0, omv m
       for (int k = 0; k < 8; k++) sum += tmp[r + k][c] * LUMA[fy][k];
       int v = (sum + 512 + (8192 << 6)) >> 10; /* shift 6+4, offset 1<<9 + OFFS<<6 */
       out[r * 4 + c] = clampi(v, 0, 1023);    /* clipPel, aux_functions.cl:403 */
+    }
+}
+
+/* ---- PROF (prediction refinement with optical flow), aux_functions.cl:215-605
+ * and the enablePROF branch of horizontal_vertical_filter_new (:1096-1239).
+ * The reference hard-codes enablePROF = 0 (affine.cl:168, :1132); vame offers
+ * it as an option (vame_set_prof), restated here from those functions. */
+
+/* aux_functions.cl:11-30 roundValue16, one component */
+static inline int round_value(int v, int shift) {
+  return (v + (1 << (shift - 1)) - (v >= 0)) >> shift;
+}
+
+/* aux_functions.cl:218-404 get{Horizontal,Vertical}DeltasPROF{2,3}Cps: the
+ * per-sample MV offsets of a 4x4 sub-block from its centre (the same for every
+ * sub-block of a CU), 1/16-pel << 8, rounded by 8 bits and clamped to +-31. */
+static void prof_deltas(const ocpmvs *cp, int nCP, int w, int h, int dH[16], int dV[16]) {
+  int lw = ilog2(w), lh = ilog2(h);
+  int hx = shl(cp->RT.x - cp->LT.x, 7 - lw), hy = shl(cp->RT.y - cp->LT.y, 7 - lw);
+  int vx, vy;
+  if (nCP == 3) {
+    vx = shl(cp->LB.x - cp->LT.x, 7 - lh);
+    vy = shl(cp->LB.y - cp->LT.y, 7 - lh);
+  } else { /* 4-parameter model: the vertical gradient is the rotated horizontal one */
+    vx = -hy;
+    vy = hx;
+  }
+  int qhx = shl(hx, 2), qvx = shl(vx, 2), qhy = shl(hy, 2), qvy = shl(vy, 2);
+  int mh[16], mv[16];
+  mh[0] = shl(hx + vx, 1) - shl(qhx + qvx, 1);
+  mv[0] = shl(hy + vy, 1) - shl(qhy + qvy, 1);
+  for (int c = 1; c < 4; c++) {
+    mh[c] = mh[c - 1] + qhx;
+    mv[c] = mv[c - 1] + qhy;
+  }
+  for (int r = 1; r < 4; r++)
+    for (int c = 0; c < 4; c++) {
+      mh[r * 4 + c] = mh[(r - 1) * 4 + c] + qvx;
+      mv[r * 4 + c] = mv[(r - 1) * 4 + c] + qvy;
+    }
+  for (int i = 0; i < 16; i++) {
+    dH[i] = clampi(round_value(mh[i], 8), -31, 31);
+    dV[i] = clampi(round_value(mv[i], 8), -31, 31);
+  }
+}
+
+/* horizontal_vertical_filter_new with applyPROF (aux_functions.cl:1096-1239):
+ * the vertical pass is not the last one (shift 6, no offset, no clip), then
+ * PROF (aux_functions.cl:471-605): the 4x4 block padded to 6x6 with reference
+ * samples around the integer position nearest the fractional one, scaled to
+ * the internal precision ((s << 4) - 8192); gradients of the >> 6 samples;
+ * dI = gx*dH + gy*dV clamped to [-8192, 8191]; (p + dI + 8 + 8192) >> 4,
+ * clipped to 10 bits. */
+static void predict_4x4_prof(const uint16_t *ref, int W, int H, int x0, int y0, omv mv,
+                             const int dH[16], const int dV[16], int out[16]) {
+  int ix = mv.x >> 4, fx = mv.x & 15, iy = mv.y >> 4, fy = mv.y & 15;
+  int bx = x0 + ix - 3, by = y0 + iy - 3; /* 11x11 window origin */
+#define WIN(r, c) ((int)ref[(size_t)clampi(by + (r), 0, H - 1) * W + clampi(bx + (c), 0, W - 1)])
+  int tmp[11][4];
+  for (int r = 0; r < 11; r++)
+    for (int c = 0; c < 4; c++) {
+      int sum = 0;
+      for (int k = 0; k < 8; k++) sum += WIN(r, c + k) * LUMA[fx][k];
+      tmp[r][c] = (sum + (-8192 * 4)) >> 2;
+    }
+  int P[6][6]; /* padded block; corners unused */
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) {
+      int sum = 0;
+      for (int k = 0; k < 8; k++) sum += tmp[r + k][c] * LUMA[fy][k];
+      P[r + 1][c + 1] = sum >> 6; /* not last: shift IF_FILTER_PREC, offset 0 */
+    }
+  const int xo = fx >> 3, yo = fy >> 3; /* aux_functions.cl:491-492 */
+  for (int k = 0; k < 4; k++) {       /* columns left / right of the block */
+    P[k + 1][0] = (WIN(3 + yo + k, 2 + xo) << 4) - 8192;
+    P[k + 1][5] = (WIN(3 + yo + k, 7 + xo) << 4) - 8192;
+  }
+  for (int k = 0; k < 6; k++) { /* rows above / below */
+    P[0][k] = (WIN(2 + yo, 2 + xo + k) << 4) - 8192;
+    P[5][k] = (WIN(7 + yo, 2 + xo + k) << 4) - 8192;
+  }
+#undef WIN
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) {
+      int gx = (P[r + 1][c + 2] >> 6) - (P[r + 1][c] >> 6);
+      int gy = (P[r + 2][c + 1] >> 6) - (P[r][c + 1] >> 6);
+      int di = clampi(gx * dH[r * 4 + c] + gy * dV[r * 4 + c], -8192, 8191);
+      out[r * 4 + c] = clampi((P[r + 1][c + 1] + di + 8 + 8192) >> 4, 0, 1023);
     }
 }
 
@@ -366,7 +455,7 @@ static ocpmvs seed_3cp(ocpmvs prev, int w, int h, int cux, int cuy, int W, int H
 
 /* One candidate CU: the whole iteration loop of affine.cl:195-917. */
 static void run_cu(const uint16_t *ref, const uint16_t *cur, int W, int H, float lambda,
-                   int nCP, int extra, int cux, int cuy, int w, int h, ocpmvs init,
+                   int nCP, int extra, int prof, int cux, int cuy, int w, int h, ocpmvs init,
                    int64_t *out_cost, ocpmvs *out_cp, int16_t *pred, int16_t *gx,
                    int16_t *gy) {
   const int inframe = (cux + w <= W) && (cuy + h <= H);
@@ -377,11 +466,17 @@ static void run_cu(const uint16_t *ref, const uint16_t *cur, int W, int H, float
   for (int it = 0; it <= niter; it++) {
     int64_t satd = 0;
     if (inframe) {
+      int dH[16], dV[16];
+      if (prof) prof_deltas(&curr, nCP, w, h, dH, dV);
       for (int sy = 0; sy < h; sy += 4)
         for (int sx = 0; sx < w; sx += 4) {
-          omv mv = subblock_mv(&curr, nCP, w, h, sx, sy, cux, cuy, W, H);
+          int spread;
+          omv mv = subblock_mv(&curr, nCP, w, h, sx, sy, cux, cuy, W, H, &spread);
           int p[16], o[16];
-          predict_4x4(ref, W, H, cux + sx, cuy + sy, mv, p);
+          if (prof && !spread) /* applyPROF = enablePROF && !isSpread (aux_functions.cl:1101) */
+            predict_4x4_prof(ref, W, H, cux + sx, cuy + sy, mv, dH, dV, p);
+          else
+            predict_4x4(ref, W, H, cux + sx, cuy + sy, mv, p);
           for (int r = 0; r < 4; r++)
             for (int c = 0; c < 4; c++) {
               o[r * 4 + c] = cur[(size_t)(cuy + sy + r) * W + cux + sx + c];
@@ -482,9 +577,9 @@ int vame_oracle_cus_per_ctu(int align) { return align ? 284 : 201; }
  * align 0 = FULL (aligned), 1 = HALF.  prev (nCP==3 only): the same-alignment
  * 2-CP result of this (POC, ref), indexed like the outputs.  Outputs are
  * indexed ctu*{201|284} + STRIDE[group] + cuIdx (affine.cl:936, :1929). */
-int vame_oracle_affine_me(const uint16_t *ref, const uint16_t *cur, int W, int H,
-                          float lambda, int align, int nCP, int extra,
-                          const ocpmvs *prev, int64_t *cost, ocpmvs *cpmvs, int nthreads) {
+int vame_oracle_affine_me_ex(const uint16_t *ref, const uint16_t *cur, int W, int H,
+                             float lambda, int align, int nCP, int extra, int prof,
+                             const ocpmvs *prev, int64_t *cost, ocpmvs *cpmvs, int nthreads) {
   int nCtus = vame_oracle_num_ctus(W, H);
   if (!nCtus || (nCP != 2 && nCP != 3) || (align != 0 && align != 1) || extra < 0) return -1;
   if (nCP == 3 && !prev) return -2;
@@ -520,7 +615,7 @@ int vame_oracle_affine_me(const uint16_t *ref, const uint16_t *cur, int W, int H
         ocpmvs init;
         memset(&init, 0, sizeof(init));
         if (nCP == 3) init = seed_3cp(prev[idx], w, h, ctuX + cx, ctuY + cy, W, H);
-        run_cu(ref, cur, W, H, lambda, nCP, extra, ctuX + cx, ctuY + cy, w, h, init,
+        run_cu(ref, cur, W, H, lambda, nCP, extra, prof, ctuX + cx, ctuY + cy, w, h, init,
                &cost[idx], &cpmvs[idx], pred, gx, gy);
       }
     }
@@ -529,7 +624,23 @@ int vame_oracle_affine_me(const uint16_t *ref, const uint16_t *cur, int W, int H
   return 0;
 }
 
+/* The reference's launch (PROF off, as affine.cl hard-codes it). */
+int vame_oracle_affine_me(const uint16_t *ref, const uint16_t *cur, int W, int H,
+                          float lambda, int align, int nCP, int extra,
+                          const ocpmvs *prev, int64_t *cost, ocpmvs *cpmvs, int nthreads) {
+  return vame_oracle_affine_me_ex(ref, cur, W, H, lambda, align, nCP, extra, 0, prev, cost,
+                                  cpmvs, nthreads);
+}
+
 /* ---- known-answer hooks for tests (each wraps one helper above) ---- */
+void vame_oracle_prof_deltas(const ocpmvs *cp, int nCP, int w, int h, int *dH16, int *dV16) {
+  prof_deltas(cp, nCP, w, h, dH16, dV16);
+}
+void vame_oracle_predict_4x4_prof(const uint16_t *ref, int W, int H, int x0, int y0, int mvx,
+                                  int mvy, const int *dH16, const int *dV16, int *out16) {
+  omv m = {mvx, mvy};
+  predict_4x4_prof(ref, W, H, x0, y0, m, dH16, dV16, out16);
+}
 int vame_oracle_satd4x4(const int *orig16, const int *pred16) { return satd4x4(orig16, pred16); }
 int vame_oracle_eg_bits(int v) { return eg_bits(v); }
 int vame_oracle_to_quarter(int v) { return to_quarter(v); }

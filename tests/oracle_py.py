@@ -32,6 +32,14 @@ def lib():
                                             ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P,
                                             ctypes.c_int]
         L.vame_oracle_affine_me.restype = ctypes.c_int
+        L.vame_oracle_affine_me_ex.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                               ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, P, P, P, ctypes.c_int]
+        L.vame_oracle_affine_me_ex.restype = ctypes.c_int
+        L.vame_oracle_prof_deltas.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
+        L.vame_oracle_predict_4x4_prof.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                   P, P, P]
         L.vame_oracle_num_ctus.argtypes = [ctypes.c_int, ctypes.c_int]
         L.vame_oracle_satd4x4.argtypes = [P, P]
         L.vame_oracle_eg_bits.argtypes = [ctypes.c_int]
@@ -55,8 +63,10 @@ def ptr(a: np.ndarray):
 
 
 def affine_me(ref: np.ndarray, cur: np.ndarray, lam: float, align: int, ncp: int,
-              extra: int = 0, prev: np.ndarray | None = None, nthreads: int = 0):
-    """One reference launch (affine.cl:11 / :960 with -DnCP=ncp) on the CPU."""
+              extra: int = 0, prev: np.ndarray | None = None, nthreads: int = 0,
+              prof: bool = False):
+    """One reference launch (affine.cl:11 / :960 with -DnCP=ncp) on the CPU;
+    prof=True turns on the reference's (hard-disabled) PROF branch."""
     H, W = ref.shape
     ref = np.ascontiguousarray(ref, dtype=np.uint16)
     cur = np.ascontiguousarray(cur, dtype=np.uint16)
@@ -64,24 +74,44 @@ def affine_me(ref: np.ndarray, cur: np.ndarray, lam: float, align: int, ncp: int
     cost = np.zeros(n, np.int64)
     cp = np.zeros(n, CPMVS_DTYPE)
     pv = None if prev is None else np.ascontiguousarray(prev)
-    rc = lib().vame_oracle_affine_me(ptr(ref), ptr(cur), W, H, lam, align, ncp, extra,
-                                     None if pv is None else ptr(pv), ptr(cost), ptr(cp),
-                                     nthreads)
+    rc = lib().vame_oracle_affine_me_ex(ptr(ref), ptr(cur), W, H, lam, align, ncp, extra,
+                                        int(prof), None if pv is None else ptr(pv),
+                                        ptr(cost), ptr(cp), nthreads)
     if rc != 0:
         raise RuntimeError(f"oracle rc={rc}")
     return cost, cp
 
 
-def affine_me_pair(ref, cur, lam, extra=0, modes=(2, 3), nthreads=0):
+def affine_me_pair(ref, cur, lam, extra=0, modes=(2, 3), nthreads=0, prof=False):
     """All four reference launches of one (POC, ref) pair, chained like
     main.cpp:759-966.  Returns {(align, ncp): (cost, cpmvs)}."""
     out = {}
     for align in (0, 1):
-        c2, p2 = affine_me(ref, cur, lam, align, 2, extra, nthreads=nthreads)
+        c2, p2 = affine_me(ref, cur, lam, align, 2, extra, nthreads=nthreads, prof=prof)
         out[(align, 2)] = (c2, p2)
         if 3 in modes:
             out[(align, 3)] = affine_me(ref, cur, lam, align, 3, extra, prev=p2,
-                                        nthreads=nthreads)
+                                        nthreads=nthreads, prof=prof)
+    return out
+
+
+def prof_deltas(cp: np.ndarray, ncp: int, w: int, h: int):
+    """aux_functions.cl:218-404: (dH[16], dV[16]) of a CU's sub-blocks."""
+    cp = np.ascontiguousarray(cp, CPMVS_DTYPE)
+    dh, dv = np.zeros(16, np.int32), np.zeros(16, np.int32)
+    lib().vame_oracle_prof_deltas(ptr(cp), ncp, w, h, ptr(dh), ptr(dv))
+    return dh, dv
+
+
+def predict_4x4_prof(ref: np.ndarray, x0: int, y0: int, mvx: int, mvy: int, dh, dv):
+    """horizontal_vertical_filter_new with enablePROF=1, isSpread=0."""
+    H, W = ref.shape
+    ref = np.ascontiguousarray(ref, dtype=np.uint16)
+    dh = np.ascontiguousarray(dh, np.int32)
+    dv = np.ascontiguousarray(dv, np.int32)
+    out = np.zeros(16, np.int32)
+    lib().vame_oracle_predict_4x4_prof(ptr(ref), W, H, x0, y0, mvx, mvy, ptr(dh), ptr(dv),
+                                       ptr(out))
     return out
 
 

@@ -16,7 +16,7 @@ from vame.synth import synth_sequence, write_csv
 import oracle_log as OL
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-GOLDEN = sorted(glob.glob(os.path.join(REPO, "tests", "golden", "*.npz")))
+GOLDEN = sorted(glob.glob(os.path.join(REPO, "tests", "golden", "s*_*.npz")))  # pair fixtures (s416_*, s832_*)
 CLI = os.path.join(REPO, "vvc-affine-gpu_amd", "bin", "vame")
 MODES = ("FULL_2CP", "FULL_3CP", "HALF_2CP", "HALF_3CP")
 

@@ -9,7 +9,7 @@ import pytest
 
 import oracle_py as O
 
-GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "s*_*.npz")))  # pair fixtures (s416_*, s832_*)
 TAGS = {"FULL_2CP": (0, 2), "FULL_3CP": (0, 3), "HALF_2CP": (1, 2), "HALF_3CP": (1, 3)}
 
 
@@ -147,3 +147,28 @@ def test_oracle_deterministic_across_threads():
     b = O.affine_me(z["ref"], z["cur"], float(z["lam"]), 1, 2, nthreads=4)
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(cpmv6(a[1]), cpmv6(b[1]))
+
+
+def test_prof_matches_reference_functions():
+    """PROF (the reference's hard-disabled branch, affine.cl:168): the oracle's
+    deltas and PROF prediction against the reference's own functions
+    (aux_functions.cl:218-605, :1096-1239) run on MI355X through
+    oracle/prof_kat.cl (tests/golden/make_prof_golden.py): 4,096 cases, 2/3 CP,
+    every CU size, every fractional phase, ~1/16 with isSpread (PROF skipped)."""
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "prof_kat.npz"))
+    win, prm = z["win"], z["prm"]
+    for g in range(len(prm)):
+        q = [int(v) for v in prm[g]]
+        cp = np.zeros(1, O.CPMVS_DTYPE)
+        for f, v in zip(("nCPs", "LTx", "LTy", "RTx", "RTy", "LBx", "LBy"), q[:7]):
+            cp[f] = v
+        dh, dv = O.prof_deltas(cp, q[0], q[7], q[8])
+        np.testing.assert_array_equal(dh, z["dH"][g], err_msg=f"case {g}")
+        np.testing.assert_array_equal(dv, z["dV"][g], err_msg=f"case {g}")
+        frame = win[g].reshape(11, 11).astype(np.uint16)  # window == frame, block at (3, 3)
+        if q[11]:  # isSpread: applyPROF = 0, the plain prediction
+            out = np.zeros(16, np.int32)
+            O.lib().vame_oracle_predict_4x4(O.ptr(frame), 11, 11, 3, 3, q[9], q[10], O.ptr(out))
+        else:
+            out = O.predict_4x4_prof(frame, 3, 3, q[9], q[10], dh, dv)
+        np.testing.assert_array_equal(out, z["pred"][g], err_msg=f"case {g}")
