@@ -78,6 +78,13 @@ int vame_affine_me_poc(vame_ctx* ctx, const uint16_t* cur, const uint16_t* const
                        int nrefs, float lambda, int mode_mask, int extra_grad_iter,
                        const vame_poc_result* out, void* stream);
 
+/* PROF (prediction refinement with optical flow).  The reference carries the
+ * code but hard-disables it (`int enablePROF=0`, affine.cl:168 / :1132;
+ * aux_functions.cl:215-605, :1096-1239); enable != 0 turns it on for the
+ * context's later launches (both entry points), exactly as the reference's
+ * functions compute it with enablePROF = 1.  Default off = reference behaviour. */
+int vame_set_prof(vame_ctx* ctx, int enable);
+
 /* Device-side kernel timing (the reference's per-PRED kernelExecutionTime,
  * main.cpp:856-866): when enabled, every kernel launch is bracketed by hipEvents
  * on the stream it runs on.  kernel_class 0 = quadrant work items

@@ -22,14 +22,15 @@ CLI = os.path.join(REPO, "vvc-affine-gpu_amd", "bin", "vame")
 PREDS = {(0, 2): 0, (0, 3): 1, (1, 2): 2, (1, 3): 3}
 
 
-def expected_logs(d, orig, recon, qp, extra=0, modes=(2, 3)):
+def expected_logs(d, orig, recon, qp, extra=0, modes=(2, 3), prof=False):
     """Oracle results -> restated writer, in the reference host's order."""
     n, H, W = orig.shape
     pre = str(d / "log")
     for poc in range(1, n + 1):
         lam = lambda_for_poc(qp, poc)
         for r, label in enumerate(ref_list(poc)):
-            res = O.affine_me_pair(recon[label], orig[poc - 1], lam, extra=extra, modes=modes)
+            res = O.affine_me_pair(recon[label], orig[poc - 1], lam, extra=extra, modes=modes,
+                                   prof=prof)
             for (align, ncp), pred in sorted(PREDS.items(), key=lambda kv: kv[1]):
                 if (align, ncp) not in res:
                     continue
@@ -136,3 +137,15 @@ def test_cli_1080p_c1(tmp_path):
     assert len(files) == 40
     rows = sum(len((out / f).read_text().splitlines()) - 1 for f in files)
     assert rows == 3 * 130950  # 3 pairs x 130,950 rows (FULL + HALF, 2 + 3 CPs)
+
+
+def test_cli_prof_416(tmp_path):
+    """--prof: the logs equal the restated writer on the oracle's PROF results."""
+    orig, recon = synth_sequence(416, 240, 3, qp=27, seed=0x50F)
+    write_csv(str(tmp_path / "orig.csv"), orig)
+    write_csv(str(tmp_path / "recon.csv"), recon)
+    exp = tmp_path / "expected"
+    exp.mkdir()
+    expected_logs(exp, orig, recon, 27, prof=True)
+    out, _ = run_cli(tmp_path, 416, 240, 3, 27, ("--prof",))
+    assert len(compare_dirs(out, exp)) == 40

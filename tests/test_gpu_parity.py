@@ -137,3 +137,55 @@ def test_live_reference_1080p(engines, tmp_path):
         hc, hp = host(out[(0, name)])
         np.testing.assert_array_equal(hc, cost, err_msg=name)
         np.testing.assert_array_equal(cp6(hp), cp[:, 1:], err_msg=name)
+
+
+PROF_CASES = [p for p in GOLDEN if any(k in p for k in ("qp32_poc1", "bigmotion", "extra1", "s832"))]
+
+
+@pytest.mark.parametrize("path", PROF_CASES, ids=[os.path.basename(p)[:-4] for p in PROF_CASES])
+def test_prof_vs_oracle(engines, path):
+    """PROF on (vame_set_prof; the reference's hard-disabled branch, pinned at
+    function level by test_oracle.py::test_prof_matches_reference_functions):
+    the fused and the per-launch entry points vs the oracle with PROF, bit for
+    bit; and PROF must change results (the branch really ran)."""
+    z = np.load(path)
+    W, H = int(z["W"]), int(z["H"])
+    eng = engines(W, H)
+    lam, extra = float(z["lam"]), int(z["extra"])
+    ref, cur = dev(z["ref"]), dev(z["cur"])
+    want = O.affine_me_pair(z["ref"], z["cur"], lam, extra, prof=True)
+    eng.set_prof(True)
+    try:
+        out = eng.affine_me_poc(cur, [ref], lam, modes=3, extra=extra)
+        for name, key in MODES.items():
+            hc, hp = host(out[(0, name)])
+            oc, op = want[key]
+            np.testing.assert_array_equal(hc, oc, err_msg=f"fused {name}")
+            np.testing.assert_array_equal(cp6(hp), oracle_cp6(op), err_msg=f"fused {name}")
+        c2, p2 = eng.affine_me(ref, cur, lam, 1, 2, extra)
+        c3, p3 = eng.affine_me(ref, cur, lam, 1, 3, extra, prev=p2)
+        for (c, p), key in (((c2, p2), (1, 2)), ((c3, p3), (1, 3))):
+            hc, hp = host((c, p))
+            np.testing.assert_array_equal(hc, want[key][0], err_msg=f"launch {key}")
+            np.testing.assert_array_equal(cp6(hp), oracle_cp6(want[key][1]), err_msg=f"launch {key}")
+    finally:
+        eng.set_prof(False)
+    plain = z["FULL_2CP_cost"]
+    assert (want[(0, 2)][0] != plain).any(), "PROF left every FULL 2-CP cost unchanged"
+
+
+def test_prof_vs_oracle_720p(engines):
+    from vame import synth
+    o, r = synth.synth_sequence(1280, 720, 2, 27)
+    eng = engines(1280, 720)
+    lam = 35.0
+    eng.set_prof(True)
+    try:
+        out = eng.affine_me_poc(dev(o[1]), [dev(r[0])], lam, modes=3)
+    finally:
+        eng.set_prof(False)
+    want = O.affine_me_pair(r[0], o[1], lam, prof=True)
+    for name, key in MODES.items():
+        hc, hp = host(out[(0, name)])
+        np.testing.assert_array_equal(hc, want[key][0], err_msg=name)
+        np.testing.assert_array_equal(cp6(hp), oracle_cp6(want[key][1]), err_msg=name)

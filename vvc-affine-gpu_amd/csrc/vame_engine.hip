@@ -46,6 +46,8 @@ struct vame_ctx {
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   // optional per-kernel timing: (start, end) event pairs per kernel class
   bool timing = false;
+  // PROF on (vame_set_prof): the *_prof kernels
+  bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];
   size_t evUsed[2] = {0, 0};
 };
@@ -251,7 +253,10 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     kb.nItems = c->nBig;
     const unsigned grid = (unsigned)(kb.nItems * kb.nCtus * kb.nRefs);
     VAME_TRY(time_begin(c, 1, sBig));
-    hipLaunchKernelGGL(affine_me_ctu, dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig, kb);
+    if (c->prof)
+      hipLaunchKernelGGL(affine_me_ctu_prof, dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig, kb);
+    else
+      hipLaunchKernelGGL(affine_me_ctu, dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig, kb);
     VAME_HIP(hipGetLastError());
     VAME_TRY(time_end(c, 1, sBig));
     return VAME_OK;
@@ -262,7 +267,10 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
     const unsigned grid = (unsigned)(kq.nItems * kq.nCtus * kq.nRefs);
     VAME_TRY(time_begin(c, 0, sQuad));
-    hipLaunchKernelGGL(affine_me_quad, dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad, kq);
+    if (c->prof)
+      hipLaunchKernelGGL(affine_me_quad_prof, dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad, kq);
+    else
+      hipLaunchKernelGGL(affine_me_quad, dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad, kq);
     VAME_HIP(hipGetLastError());
     VAME_TRY(time_end(c, 0, sQuad));
     return VAME_OK;
@@ -422,6 +430,12 @@ int vame_affine_me_poc(vame_ctx* c, const uint16_t* cur, const uint16_t* const* 
     }
   }
   return launch(c, kp, true, true, true, (hipStream_t)stream);
+}
+
+int vame_set_prof(vame_ctx* c, int enable) {
+  if (!c) return VAME_E_INVALID;
+  c->prof = enable != 0;
+  return VAME_OK;
 }
 
 int vame_set_timing(vame_ctx* c, int enable) {

@@ -472,12 +472,67 @@ __device__ __forceinline__ int satd_4x4(const uint2 (&O)[4], const uint2 (&P)[4]
   return (sum + 1) >> 1;
 }
 
+// PROF, the reference's hard-disabled refinement (enablePROF = 0 at
+// affine.cl:168 / :1132), offered as an option (vame_set_prof).  Per sample,
+// the MV offset from the sub-block centre (aux_functions.cl:218-404,
+// get{Horizontal,Vertical}DeltasPROF{2,3}Cps), linear in (r, c) before its
+// rounding: m(r, c) = 2 (h + v) - 2 (4h + 4v) + 4h c + 4v r, rounded by 8 bits
+// (roundValue16) and clamped to +-31.  Recomputed per sample from six
+// registers instead of holding 32 deltas.
+__device__ __forceinline__ int prof_delta(int base, int q4h, int q4v, int r, int c) {
+  const int m = base + q4h * c + q4v * r;
+  return clampi((m + 128 - (m >= 0)) >> 8, -31, 31);
+}
+// PROF proper (aux_functions.cl:471-605) on the vertical pass taken as not
+// the last one (shift 6, no offset, no clip: aux_functions.cl:1163-1174):
+// the block padded to 6x6 with the reference samples around the integer
+// position nearest the fractional MV (xFrac >> 3, yFrac >> 3), scaled to the
+// internal precision, gradients of the >> 6 samples, dI = gx dH + gy dV
+// clamped to [-8192, 8191], then (p + dI + 8 + 8192) >> 4 clipped to 10 bits.
+// acc holds the vertical sums + 524800 (the re-based filter offsets);
+// smp(row, col) reads the 9x9 filter window (origin two samples above-left
+// of the integer-MV corner).
+template <typename Smp>
+__device__ __forceinline__ void prof_refine(const int (&acc)[4][4], const MvField& f, int fx, int fy,
+                                            Smp smp, int (&pr)[4][4]) {
+  const int xo = fx >> 3, yo = fy >> 3;
+  int L[4], R[4], T[4], B[4];  // padding columns / rows, >> 6 of the scaled samples
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    L[k] = ((smp(yo + 2 + k, xo + 1) << 4) - 8192) >> 6;
+    R[k] = ((smp(yo + 2 + k, xo + 6) << 4) - 8192) >> 6;
+    T[k] = ((smp(yo + 1, xo + 2 + k) << 4) - 8192) >> 6;
+    B[k] = ((smp(yo + 6, xo + 2 + k) << 4) - 8192) >> 6;
+  }
+  int p[4][4], q[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      p[r][c] = (acc[r][c] - 524800) >> 6;
+      q[r][c] = p[r][c] >> 6;
+    }
+  const int q4hx = shl(f.hx, 2), q4vx = shl(f.vx, 2), q4hy = shl(f.hy, 2), q4vy = shl(f.vy, 2);
+  const int bh = shl(f.hx + f.vx, 1) - shl(q4hx + q4vx, 1);
+  const int bv = shl(f.hy + f.vy, 1) - shl(q4hy + q4vy, 1);
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int gx = (c == 3 ? R[r] : q[r][c + 1]) - (c == 0 ? L[r] : q[r][c - 1]);
+      const int gy = (r == 3 ? B[c] : q[r + 1][c]) - (r == 0 ? T[c] : q[r - 1][c]);
+      const int di = clampi(gx * prof_delta(bh, q4hx, q4vx, r, c) + gy * prof_delta(bv, q4hy, q4vy, r, c),
+                            -8192, 8191);
+      pr[r][c] = clampi((p[r][c] + di + 8 + 8192) >> 4, 0, 1023);
+    }
+}
+
 // One 4x4 sub-block: affine MV (affine.cl:215-252), 9x9 window with
 // clamp-to-edge (affine.cl:254-326), separable 6-tap filter (aux_functions.cl
 // :1096-1239, PROF off), SATD against the original (aux_functions.cl:1940-2043).
 // The prediction stays in registers (P[r] = packed sample pairs of row r) for
 // the gradient step, and so do the original samples (O[r]).
-template <int TILE, int TP>
+template <int TILE, int TP, bool PROF>
 __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, const Geo& g,
                                           const uint16_t* s_tile, int tx0, int ty0,
                                           const uint16_t* __restrict__ ref,
@@ -518,10 +573,23 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
                        acc);
   }
   int pr[4][4];
+  if (PROF && !f.spread) {  // applyPROF = enablePROF && !isSpread (aux_functions.cl:1101)
+    if (inTile) {
+      const uint16_t* win = s_tile + ty * TP + tx;
+      prof_refine(acc, f, fx, fy, [&](int r, int c) { return (int)win[r * TP + c]; }, pr);
+    } else {
+      prof_refine(acc, f, fx, fy,
+                  [&](int r, int c) {
+                    return (int)ref[(size_t)clampi(wy + r, 0, H - 1) * W + clampi(wx + c, 0, W - 1)];
+                  },
+                  pr);
+    }
+  } else {
 #pragma unroll
-  for (int r = 0; r < 4; r++)
+    for (int r = 0; r < 4; r++)
 #pragma unroll
-    for (int c = 0; c < 4; c++) pr[r][c] = clampi(acc[r][c] >> 10, 0, 1023);  // clipPel
+      for (int c = 0; c < 4; c++) pr[r][c] = clampi(acc[r][c] >> 10, 0, 1023);  // clipPel
+  }
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     P[r].x = pack16(pr[r][0], pr[r][1]);
@@ -1057,7 +1125,7 @@ __device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v
 }
 
 
-template <int REGION>
+template <int REGION, bool PROF>
 __device__ __forceinline__ void affine_me_body(const KParams& p) {
   using C = Cfg<REGION>;
   __shared__ __attribute__((aligned(16))) uint16_t s_tile[C::TILE_ELEMS];
@@ -1256,13 +1324,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         int cp[6];
         for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
         const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
-        const int satdLane = predict_sb<C::TILE, C::TP>(f, sxp, syp, gp, s_tile, tx0, ty0, ref, cur,
+        const int satdLane = predict_sb<C::TILE, C::TP, PROF>(f, sxp, syp, gp, s_tile, tx0, ty0, ref, cur,
                                                         W, H, s_coef, Pr, Og);
         if (VAME_DUP & 1) {
           MvField f2 = f;
           opaque(f2.bx);
           uint2 P2[4], O2[4];
-          int s2 = predict_sb<C::TILE, C::TP>(f2, sxp, syp, gp, s_tile, tx0, ty0, ref, cur, W, H,
+          int s2 = predict_sb<C::TILE, C::TP, PROF>(f2, sxp, syp, gp, s_tile, tx0, ty0, ref, cur, W, H,
                                               s_coef, P2, O2);
           s2 += (int)(P2[0].x ^ P2[3].y ^ O2[1].x);
           asm volatile("" ::"v"(s2));
@@ -1461,10 +1529,16 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 // VGPRs at 128 to let all 16 waves be resident.
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad(
     KParams p) {
-  affine_me_body<64>(p);
+  affine_me_body<64, false>(p);
 }
 // 128-class items: one 1024-thread workgroup per CU (94 KB of LDS), one lane
 // per sub-block of a 128x128 CU.
-__global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_body<128>(p); }
+__global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_body<128, false>(p); }
+// The same with PROF (vame_set_prof).
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad_prof(
+    KParams p) {
+  affine_me_body<64, true>(p);
+}
+__global__ __launch_bounds__(1024) void affine_me_ctu_prof(KParams p) { affine_me_body<128, true>(p); }
 
 }  // namespace vame

@@ -13,6 +13,8 @@
 //                             does (per-PRED kernel times); default = fused
 //                             per-POC launch (vame_affine_me_poc)
 //               --threads T   host threads for CSV parsing / log formatting
+//               --prof        PROF on (the reference hard-disables it,
+//                             affine.cl:168; vame_set_prof)
 //
 // Differences to the reference host, all deliberate:
 //  * the 4-slot reference ring (main.cpp:591-707) is label bookkeeping only:
@@ -99,6 +101,8 @@ void print_help(Cli& c) {
   }
   printf("%-40s%s\n", "  --per-launch",
          "one launch per (refIdx, PRED) like the reference (per-PRED kernel times)");
+  printf("%-40s%s\n", "  --prof",
+         "PROF on (the reference's enablePROF, hard-coded 0 there)");
 }
 
 // Returns 0 ok, 1 help, 2 error.
@@ -117,7 +121,7 @@ int parse(Cli& c, int argc, char** argv) {
         have_val = true;
       }
       if (n == "help") return 1;
-      if (n == "per-launch") {
+      if (n == "per-launch" || n == "prof") {
         c.flags_set.push_back(n);
         continue;
       }
@@ -275,6 +279,7 @@ struct Shared {
 struct Job {
   int device, W, H, nCtus, qp, extra, mode_mask;
   bool per_launch;
+  bool prof;
   std::vector<int> pocs;
   const uint16_t* orig;   // host, POC p at frame p-1
   const uint16_t* recon;  // host, POC p at frame p
@@ -313,6 +318,7 @@ void gpu_worker(Job J) {
   GPU_CHECK(hipSetDevice(J.device), "hipSetDevice");
   vame_ctx* ctx = nullptr;
   VAME_CHECK(vame_create(&ctx, J.device, J.W, J.H), "vame_create");
+  VAME_CHECK(vame_set_prof(ctx, J.prof ? 1 : 0), "vame_set_prof");
   hipStream_t st;
   GPU_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
   const size_t fsz = (size_t)J.W * J.H;
@@ -620,6 +626,7 @@ int main(int argc, char** argv) {
     j.extra = extra;
     j.mode_mask = mode_mask;
     j.per_launch = per_launch;
+    j.prof = std::find(c.flags_set.begin(), c.flags_set.end(), "prof") != c.flags_set.end();
     j.orig = orig.data();
     j.recon = recon.data();
     j.L = &L;

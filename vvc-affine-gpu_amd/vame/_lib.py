@@ -14,7 +14,7 @@ EXPORTS = (
     "vame_cus_per_ctu", "vame_num_groups", "vame_group_geometry", "vame_lambda", "vame_poc_qp",
     "vame_ref_list", "vame_strerror", "vame_last_hip_error", "vame_version", "vame_set_timing",
     "vame_get_timing", "vame_read_frames", "vame_log_remove_old", "vame_log_write_headers",
-    "vame_log_append", "vame_log_file_count",
+    "vame_log_append", "vame_log_file_count", "vame_set_prof",
 )
 
 
@@ -54,6 +54,7 @@ def lib():
         L.vame_last_hip_error.restype = ctypes.c_char_p
         L.vame_version.restype = ctypes.c_char_p
         L.vame_set_timing.argtypes = [P, I]
+        L.vame_set_prof.argtypes = [P, I]
         L.vame_get_timing.argtypes = [P, I, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_int), I]
         C = ctypes.c_char_p

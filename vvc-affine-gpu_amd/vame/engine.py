@@ -49,6 +49,11 @@ class Engine:
         except Exception:
             pass
 
+    def set_prof(self, enable: bool) -> None:
+        """PROF on/off for later launches (the reference hard-disables it,
+        affine.cl:168); vame_set_prof."""
+        check(lib().vame_set_prof(self._h, int(enable)))
+
     def set_timing(self, enable: bool) -> None:
         check(lib().vame_set_timing(self._h, int(enable)))
 
