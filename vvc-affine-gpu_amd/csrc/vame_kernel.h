@@ -40,7 +40,6 @@ namespace vame {
 
 constexpr int kMaxCu = 16;    // CU slots per work item
 constexpr int kMaxWaves = 4;
-constexpr int kMargin = 16;   // LDS reference-tile margin around the work-item region
 constexpr int kThreads = 256;  // quadrant workgroups
 constexpr int kNumMom = 24;   // 3 CP: {1,u,v,uu,uv,vv} x {xx,xy,yy} + {1,u,v} x {xe,ye}
 constexpr int kNumVal2 = 14;  // 2 CP: 10 distinct matrix entries + 4 right-hand sides
@@ -104,6 +103,14 @@ struct KParams {
 // system).
 #ifndef VAME_DUP
 #define VAME_DUP 0
+#endif
+// quadrant kernel occupancy target (waves per SIMD; caps the VGPRs)
+#ifndef VAME_WAVES
+#define VAME_WAVES 4
+#endif
+// LDS reference-tile margin of the quadrant kernel (samples)
+#ifndef VAME_QMARGIN
+#define VAME_QMARGIN 16
 #endif
 
 // VAME_PHASE_TIMING (profiling-only builds, libvame_phase.so): every wave sums
@@ -365,31 +372,24 @@ __device__ __forceinline__ void vpair(int k, const int (&t0)[4], const int (&t1)
     }
   }
 }
-// Window rows from the LDS tile, software-pipelined one row pair ahead (the
-// scheduling barriers keep the compiler from hoisting all 45 reads, which
-// would cost ~40 VGPRs of occupancy).
+// Window rows from the LDS tile, one row pair at a time (software-pipelining
+// the reads one pair ahead held ~20 more VGPRs for no measurable gain: the
+// other waves hide the LDS latency).
 template <int PITCH_DW>
 __device__ __forceinline__ void filter_rows(const unsigned* src, const uint4& KA, const uint4& KB,
                                             const uint4& G0, const uint4& G1, int (&acc)[4][4]) {
-  unsigned D[2][2][5];
-#pragma unroll
-  for (int h = 0; h < 2; h++)
-#pragma unroll
-    for (int q = 0; q < 5; q++) D[0][h][q] = src[h * PITCH_DW + q];
 #pragma unroll
   for (int k = 0; k < 5; k++) {
-    const int cb = k & 1, nb = cb ^ 1;
-    if (k < 4) {  // prefetch row pair k + 1 (row 9 does not exist)
+    unsigned E[2][5];
 #pragma unroll
-      for (int h = 0; h < 2; h++)
-        if (2 * (k + 1) + h < 9) {
+    for (int h = 0; h < 2; h++)
+      if (2 * k + h < 9) {  // row 9 does not exist
 #pragma unroll
-          for (int q = 0; q < 5; q++) D[nb][h][q] = src[(2 * (k + 1) + h) * PITCH_DW + q];
-        }
-    }
+        for (int q = 0; q < 5; q++) E[h][q] = src[(2 * k + h) * PITCH_DW + q];
+      }
     int t0[4], t1[4] = {0, 0, 0, 0};
-    hrow_raw(D[cb][0], KA, KB, t0);
-    if (k < 4) hrow_raw(D[cb][1], KA, KB, t1);
+    hrow_raw(E[0], KA, KB, t0);
+    if (k < 4) hrow_raw(E[1], KA, KB, t1);
     vpair(k, t0, t1, G0, G1, acc);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -552,6 +552,23 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   const int wx = g.x + sx + ix - 2, wy = g.y + sy + iy - 2;  // window origin (frame)
   const int tx = wx - tx0, ty = wy - ty0;
   const bool inTile = (unsigned)tx <= (unsigned)(TILE - 9) && (unsigned)ty <= (unsigned)(TILE - 9);
+  if (!PROF && __builtin_amdgcn_ballot_w64(!(inTile && (fx | fy) == 0)) == 0) {
+    // Every active lane has an integer MV inside the tile (e.g. every sub-block
+    // of the first 2-CP prediction, from zero CPMVs): the phase-0 filter is the
+    // identity -- (64 s - 32768) >> 2 = 16 s - 8192, then
+    // (64 (16 s - 8192) + 512 + (8192 << 6)) >> 10 = s, within [0, 1023] (KAT-1)
+    // -- so the prediction is the window's inner 4x4, copied from the tile.
+    const int i0 = (ty + 2) * TP + tx + 2;  // the block's first sample in the tile
+    const unsigned* s32 = reinterpret_cast<const unsigned*>(s_tile) + (i0 >> 1);
+    const unsigned sh = (unsigned)(i0 & 1) << 4;  // 0 or 16: its half of the dword
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const unsigned d0 = s32[r * (TP / 2)], d1 = s32[r * (TP / 2) + 1], d2 = s32[r * (TP / 2) + 2];
+      P[r].x = __builtin_amdgcn_alignbit(d1, d0, sh);
+      P[r].y = __builtin_amdgcn_alignbit(d2, d1, sh);
+    }
+    return satd_4x4(O, P);
+  }
   const int sp = inTile ? (tx & 1) : 0;
   const uint4 KA = s_coef[fx * 3 + sp], KB = s_coef[fx * 3 + sp + 1];
   const uint4 G0 = s_coef[fy * 3 + 0], G1 = s_coef[fy * 3 + 1];
@@ -861,10 +878,11 @@ struct CuState {
 template <int REGION>
 struct Cfg {
   static constexpr int THREADS = REGION == 128 ? 1024 : 256;  // workgroup size = sub-blocks
-  static constexpr int TILE = REGION + 2 * kMargin;     // tile edge (samples)
+  static constexpr int MARGIN = REGION == 128 ? 16 : VAME_QMARGIN;  // reference-tile margin
+  static constexpr int TILE = REGION + 2 * MARGIN;      // tile edge (samples)
   // tile pitch (samples) == 8 (mod 16): the window rows of sub-blocks 4 rows
   // apart land 16 banks apart (2-way at most for the packed-pair reads)
-  static constexpr int TP = REGION == 128 ? 168 : 104;
+  static constexpr int TP = (TILE + 7) / 16 * 16 + 8;
   static constexpr int TILE_ELEMS = TILE * TP + 16;
   static constexpr int NSB = REGION * REGION / 16;      // sub-blocks per work item (max)
 };
@@ -1130,8 +1148,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   using C = Cfg<REGION>;
   __shared__ __attribute__((aligned(16))) uint16_t s_tile[C::TILE_ELEMS];
   static_assert((C::TP * 2) % 16 == 0 && C::TILE % 8 == 0, "16-byte tile rows");
-  __shared__ uint4 s_top[C::NSB];  // extended row 0 of every sub-block's prediction
-  __shared__ uint4 s_bot[C::NSB];  // extended row 3
+  __shared__ uint2 s_top[C::NSB];  // row 0 of every sub-block's prediction (packed pairs)
+  __shared__ uint2 s_bot[C::NSB];  // row 3
   __shared__ __attribute__((aligned(16))) long long s_val[kMaxCu][kNumMom];
   __shared__ double s_mat[kMaxCu][42];  // per CU: N x (N + 1) system, N <= 6
   __shared__ double s_mat_dup[(VAME_DUP & 16) ? kMaxCu : 1][42];
@@ -1178,7 +1196,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   const int hdr = __builtin_amdgcn_readfirstlane(s_hdr[0]);
   const int nCu = hdr & 0xFF, nWaves = (hdr >> 16) & 0xFF;
   const bool coop = ((hdr >> 8) & 0xFF) != 0;
-  const int tx0 = ctuX + s_hdr[2] - kMargin, ty0 = ctuY + s_hdr[3] - kMargin;  // tile origin
+  const int tx0 = ctuX + s_hdr[2] - C::MARGIN, ty0 = ctuY + s_hdr[3] - C::MARGIN;  // tile origin
 
   // ---- stage the reference region (+margin) into LDS, clamp-to-edge padded:
   // 16-byte chunks, every load of a thread issued before its first LDS store
@@ -1340,8 +1358,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 #pragma unroll
         for (int r = 0; r < 4; r++)
           X[r + 1] = ext_row(Pr[r], dpp32<0x138, 0xF>((int)Pr[r].y), dpp32<0x130, 0xF>((int)Pr[r].x));
-        s_top[sbIdx] = X[1];
-        s_bot[sbIdx] = X[4];
+        s_top[sbIdx] = Pr[0];
+        s_bot[sbIdx] = Pr[3];
         const int v = logS == 4 ? seg_sum_c<4>(satdLane)
                       : logS == 5 ? seg_sum_c<5>(satdLane) : seg_sum_c<6>(satdLane);
         if (leader) {
@@ -1401,8 +1419,10 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       {
         int S[5] = {0, 0, 0, 0, 0};
         if (live && !(VAME_ABLATE & 2)) {
-          X[0] = s_bot[sbTop];
-          X[5] = s_top[sbBot];
+          // the neighbours' edge rows, extended by the left / right lanes' copies
+          const uint2 tb = s_bot[sbTop], bt = s_top[sbBot];
+          X[0] = ext_row(tb, dpp32<0x138, 0xF>((int)tb.y), dpp32<0x130, 0xF>((int)tb.x));
+          X[5] = ext_row(bt, dpp32<0x138, 0xF>((int)bt.y), dpp32<0x130, 0xF>((int)bt.x));
           Geo gg = g;
           int sxg = sx, syg = sy;
           opaque_geo(gg, sxg, syg);
@@ -1527,7 +1547,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 // Distinct entry points so profiles tell the two work-item classes apart.
 // Quadrant items: 4 workgroups per CU fit the LDS (~35 KB each), so cap the
 // VGPRs at 128 to let all 16 waves be resident.
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VAME_WAVES))) void affine_me_quad(
     KParams p) {
   affine_me_body<64, false>(p);
 }
@@ -1535,7 +1555,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // per sub-block of a 128x128 CU.
 __global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_body<128, false>(p); }
 // The same with PROF (vame_set_prof).
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad_prof(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VAME_WAVES))) void affine_me_quad_prof(
     KParams p) {
   affine_me_body<64, true>(p);
 }
