@@ -538,9 +538,13 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
                                           const uint16_t* __restrict__ ref,
                                           const uint16_t* __restrict__ cur, int W, int H,
                                           const uint4* s_coef, uint2 (&P)[4], uint2 (&O)[4]) {
+  {  // 32-bit byte offsets from the uniform frame base (frames < 4 GiB): the
+     // saddr form of global_load, no 64-bit address arithmetic per row
+    const unsigned b0 = (unsigned)((g.y + sy) * W + g.x + sx) * 2u, bw = (unsigned)W * 2u;
+    const char* base = reinterpret_cast<const char*>(cur);
 #pragma unroll
-  for (int r = 0; r < 4; r++)
-    O[r] = *reinterpret_cast<const uint2*>(cur + (size_t)(g.y + sy + r) * W + g.x + sx);
+    for (int r = 0; r < 4; r++) O[r] = *reinterpret_cast<const uint2*>(base + (b0 + (unsigned)r * bw));
+  }
   const int px = f.spread ? (g.w >> 1) : sx + 2, py = f.spread ? (g.h >> 1) : sy + 2;
   // |h|, |v| < 2^22 (clamped CPMVs, << (7 - log2 size)), px, py <= 128: 24-bit products are exact
   int mx = f.bx + __mul24(f.hx, px) + __mul24(f.vx, py);
