@@ -70,6 +70,10 @@ __global__ __launch_bounds__(1024) void k(unsigned long long* cyc, int iters, un
       REP8(asm volatile("v_cmp_gt_i32_e64 s[40:41], %8, %0\n v_cmp_gt_i32_e64 s[42:43], %8, %1\n v_cmp_gt_i32_e64 s[44:45], %8, %2\n v_cmp_gt_i32_e64 s[46:47], %8, %3\n v_cmp_gt_i32_e64 s[40:41], %8, %4\n v_cmp_gt_i32_e64 s[42:43], %8, %5\n v_cmp_gt_i32_e64 s[44:45], %8, %6\n v_cmp_gt_i32_e64 s[46:47], %8, %7" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b) : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47");)
     } else if (OP == 26) {  // v_sub_u32 + v_cndmask_b32_e32 mix (1:1)
       REP8(asm volatile("v_sub_u32 %0, %0, %8\n v_cndmask_b32 %1, %1, %8, vcc\n v_sub_u32 %2, %2, %8\n v_cndmask_b32 %3, %3, %8, vcc\n v_sub_u32 %4, %4, %8\n v_cndmask_b32 %5, %5, %8, vcc\n v_sub_u32 %6, %6, %8\n v_cndmask_b32 %7, %7, %8, vcc" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b));)
+    } else if (OP == 27) {  // pairs of v_cndmask_b32_e32 (vcc) + one v_add_u32_dpp, as in the reductions
+      REP8(asm volatile("v_cndmask_b32 %0, %0, %8, vcc\n v_cndmask_b32 %1, %1, %8, vcc\n v_add_u32_dpp %2, %8, %2 row_shr:1 bound_ctrl:0\n v_cndmask_b32 %3, %3, %8, vcc\n v_cndmask_b32 %4, %4, %8, vcc\n v_add_u32_dpp %5, %8, %5 row_shr:1 bound_ctrl:0\n v_cndmask_b32 %6, %6, %8, vcc\n v_cndmask_b32 %7, %7, %8, vcc" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b));)
+    } else if (OP == 28) {  // the same with v_cndmask_b32_e64 on an SGPR pair
+      REP8(asm volatile("v_cndmask_b32_e64 %0, %0, %8, %9\n v_cndmask_b32_e64 %1, %1, %8, %9\n v_add_u32_dpp %2, %8, %2 row_shr:1 bound_ctrl:0\n v_cndmask_b32_e64 %3, %3, %8, %9\n v_cndmask_b32_e64 %4, %4, %8, %9\n v_add_u32_dpp %5, %8, %5 row_shr:1 bound_ctrl:0\n v_cndmask_b32_e64 %6, %6, %8, %9\n v_cndmask_b32_e64 %7, %7, %8, %9" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b), "s"(mask));)
     }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -107,6 +111,9 @@ void run(const char* name, int instrPerIter) {
 }
 
 int main() {
+  run<27>("2 cndmask_e32 + dpp", 64);
+  run<28>("2 cndmask_e64 + dpp", 64);
+  return 0;
   run<22>("v_cndmask_e64_vcc", 64);
   run<23>("cmp_e64+7cndmask_e64", 64);
   run<24>("v_cmp_e32_vcc", 64);

@@ -968,8 +968,20 @@ struct HalfVals {
   int v[M];
 };
 
-// lane-bit masks of the wave (the exchange partner's bit), wave-uniform
-__device__ __forceinline__ bool lane_bit(int b) { return (__lane_id() >> b) & 1; }
+// Lane-bit selects: lane l gets (l >> B) & 1 ? if1 : if0.  Issued as the VOP3
+// v_cndmask_b32 with the constant lane mask in an SGPR pair: the VOP2 form the
+// compiler picks (condition in VCC) runs ~3x slower when two follow each other
+// (profiles/ubench/valu_rate.hip: 7.7 vs 2.5 SIMD cycles per instruction in
+// the reductions' select-select-DPP pattern).
+constexpr unsigned long long kLaneBitMask[6] = {0xAAAAAAAAAAAAAAAAull, 0xCCCCCCCCCCCCCCCCull,
+                                                0xF0F0F0F0F0F0F0F0ull, 0xFF00FF00FF00FF00ull,
+                                                0xFFFF0000FFFF0000ull, 0xFFFFFFFF00000000ull};
+template <int B>
+__device__ __forceinline__ int sel_bit(int if0, int if1) {
+  int r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(kLaneBitMask[B]));
+  return r;
+}
 
 // One exchange over lane bit B via DPP: returns keep + partner(send).
 template <int B>
@@ -998,11 +1010,10 @@ __device__ __forceinline__ void halve(int* x) {
       x[j] = (int)(r[0] + r[1]);
     }
   } else {
-    const bool beta = lane_bit(B);
 #pragma unroll
     for (int j = 0; j < H; j++) {
       const int a = x[j], b = j + H < M ? x[j + H] : 0;
-      x[j] = xchg_dpp<B>(beta ? b : a, beta ? a : b);
+      x[j] = xchg_dpp<B>(sel_bit<B>(a, b), sel_bit<B>(b, a));
     }
   }
 }
@@ -1104,8 +1115,7 @@ __device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int
                              : __builtin_amdgcn_permlane16_swap((unsigned)lo, (unsigned)hi, false, false);
       x[i] = (int)(r[0] + r[1]);
     } else {
-      const bool beta = lane_bit(B0);
-      x[i] = xchg_dpp<B0>(beta ? hi : lo, beta ? lo : hi);
+      x[i] = xchg_dpp<B0>(sel_bit<B0>(lo, hi), sel_bit<B0>(hi, lo));
     }
   }
   butterfly<LOGS, 1, NV>(x);
