@@ -189,3 +189,25 @@ def test_prof_vs_oracle_720p(engines):
         hc, hp = host(out[(0, name)])
         np.testing.assert_array_equal(hc, want[key][0], err_msg=name)
         np.testing.assert_array_equal(cp6(hp), oracle_cp6(want[key][1]), err_msg=name)
+
+
+@pytest.fixture(scope="module")
+def frames_2160p():
+    from vame import synth
+    return synth.synth_sequence(3840, 2160, 1, 32, seed=0x4C4)
+
+
+@pytest.mark.parametrize("qp", [22, 37])
+def test_fused_vs_oracle_2160p(engines, frames_2160p, qp):
+    """BASELINE configs[3] shape (3840x2160, the QP sweep's ends via their
+    lambdas): one (POC 1, ref 0) pair, all four modes, bit-exact vs the oracle."""
+    from vame.hostlogic import lambda_for_poc
+    o, r = frames_2160p
+    eng = engines(3840, 2160)
+    lam = lambda_for_poc(qp, 1)
+    out = eng.affine_me_poc(dev(o[0]), [dev(r[0])], lam, modes=3)
+    want = O.affine_me_pair(r[0], o[0], lam)
+    for name, key in MODES.items():
+        hc, hp = host(out[(0, name)])
+        np.testing.assert_array_equal(hc, want[key][0], err_msg=f"QP{qp} {name}")
+        np.testing.assert_array_equal(cp6(hp), oracle_cp6(want[key][1]), err_msg=f"QP{qp} {name}")
