@@ -105,6 +105,12 @@ struct KParams {
 #define VAME_DUP 0
 #endif
 // quadrant kernel occupancy target (waves per SIMD; caps the VGPRs)
+// wave priority (s_setprio) during the latency-bound solve (0 = off): its
+// dependent FP64 / LDS chain issues ahead of other waves' prediction work
+// (~0.5 %; priority over the whole post-prediction part measured the same)
+#ifndef VAME_PRIO
+#define VAME_PRIO 3
+#endif
 #ifndef VAME_WAVES
 #define VAME_WAVES 4
 #endif
@@ -1471,6 +1477,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       PH_MARK(kPhGradient)
 
       // =============== solve + CPMV update (affine.cl:782-893), per CU segment ===============
+      if (VAME_PRIO) __builtin_amdgcn_s_setprio(VAME_PRIO);
       if (!(VAME_ABLATE & 1)) {
         // the CU's lanes in its first wave solve it together
         int cuS = myCu, loc = local;
@@ -1526,9 +1533,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           }
         }
         if (!coop) {  // leave once every CU of this wave is settled (wave-local)
-          if (__ballot(liveNew) == 0) break;
+          if (__ballot(liveNew) == 0) {
+            if (VAME_PRIO) __builtin_amdgcn_s_setprio(0);
+            break;
+          }
         }
       }
+      if (VAME_PRIO) __builtin_amdgcn_s_setprio(0);
       phase_sync(coop);
       PH_MARK(kPhSolve)
       if (coop) {  // leave once every CU of the item is settled (flags read after the sync)
