@@ -110,13 +110,16 @@ def main():
                for _ in plan]
     timing_spans = [False]
 
+    jobs = [(d_orig[poc - 1], [d_recon[r] for r in refs], lam, out) for (poc, refs, lam, out) in plan]
+
     def step():
-        for i, (poc, refs, lam, out) in enumerate(plan):
-            if timing_spans[0]:
+        if timing_spans[0]:  # per-POC launches, each bracketed by events
+            for i, job in enumerate(jobs):
                 span_ev[i][0].record()
-            eng.affine_me_poc(d_orig[poc - 1], [d_recon[r] for r in refs], lam, modes, 0, out=out)
-            if timing_spans[0]:
+                eng.affine_me_batch([job], modes, 0)
                 span_ev[i][1].record()
+        else:  # the step's POCs in shared launches (vame_affine_me_batch)
+            eng.affine_me_batch(jobs, modes, 0)
         if dist is not None:  # the one exchange step: decision-log gather over RCCL/xGMI
             shard.gather(shard.pack([pl[3] for pl in plan], words, dev), world)
 

@@ -78,6 +78,20 @@ int vame_affine_me_poc(vame_ctx* ctx, const uint16_t* cur, const uint16_t* const
                        int nrefs, float lambda, int mode_mask, int extra_grad_iter,
                        const vame_poc_result* out, void* stream);
 
+/* Batched fused call: several POCs (each one vame_affine_me_poc) in as few
+ * launches as possible (32 (POC, refIdx) pairs per launch), so consecutive
+ * POCs share one grid -- no launch gaps or tails between them.  Results are
+ * identical to one vame_affine_me_poc per job. */
+typedef struct {
+  const uint16_t* cur;              /* orig of the POC */
+  const uint16_t* const* refs;      /* its nrefs (1..4) reference frames, refIdx order */
+  int nrefs;
+  float lambda;
+  const vame_poc_result* out;
+} vame_poc_job;
+int vame_affine_me_batch(vame_ctx* ctx, const vame_poc_job* jobs, int njobs, int mode_mask,
+                         int extra_grad_iter, void* stream);
+
 /* PROF (prediction refinement with optical flow).  The reference carries the
  * code but hard-disables it (`int enablePROF=0`, affine.cl:168 / :1132;
  * aux_functions.cl:215-605, :1096-1239); enable != 0 turns it on for the

@@ -211,3 +211,29 @@ def test_fused_vs_oracle_2160p(engines, frames_2160p, qp):
         hc, hp = host(out[(0, name)])
         np.testing.assert_array_equal(hc, want[key][0], err_msg=f"QP{qp} {name}")
         np.testing.assert_array_equal(cp6(hp), oracle_cp6(want[key][1]), err_msg=f"QP{qp} {name}")
+
+
+def test_batch_equals_per_poc(engines):
+    """vame_affine_me_batch (several POCs in shared launches; 36 pairs cross the
+    32-pair launch limit) == one vame_affine_me_poc per POC == the oracle."""
+    from vame import synth
+    o, r = synth.synth_sequence(416, 240, 12, 32, seed=0xBA7C)
+    eng = engines(416, 240)
+    jobs, singles = [], []
+    for poc in range(1, 13):
+        refs = [dev(r[k]) for k in range(max(0, poc - 3), poc)][::-1]  # 1..3 refs
+        lam = 40.0 + poc
+        jobs.append((dev(o[poc - 1]), refs, lam, eng.alloc_poc(len(refs), 3)))
+        singles.append(eng.affine_me_poc(dev(o[poc - 1]), refs, lam, modes=3))
+    outs = eng.affine_me_batch(jobs, 3, 0)
+    assert sum(len(j[1]) for j in jobs) > 32
+    for poc, (out, single) in enumerate(zip(outs, singles), start=1):
+        for key in out:
+            hc, hp = host(out[key])
+            sc, sp = host(single[key])
+            np.testing.assert_array_equal(hc, sc, err_msg=f"POC{poc} {key}")
+            np.testing.assert_array_equal(hp, sp, err_msg=f"POC{poc} {key}")
+    want = O.affine_me_pair(r[11], o[11], 52.0)  # POC 12, refIdx 0 = recon 11
+    for name, key in MODES.items():
+        hc, hp = host(outs[11][(0, name)])
+        np.testing.assert_array_equal(hc, want[key][0], err_msg=name)

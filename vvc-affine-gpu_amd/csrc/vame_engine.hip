@@ -197,12 +197,11 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& quadFull,
   }
 }
 
-void fill_common(KParams& kp, const vame_ctx* c, float lambda, int extra) {
+void fill_common(KParams& kp, const vame_ctx* c, int extra) {
   kp.W = c->W;
   kp.H = c->H;
   kp.nCtus = c->nCtus;
   kp.ctusPerRow = c->ctusPerRow;
-  kp.lambda = lambda;
   kp.extra = extra;
 }
 
@@ -251,7 +250,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     KParams kb = kp;
     kb.items = c->dBig;
     kb.nItems = c->nBig;
-    const unsigned grid = (unsigned)(kb.nItems * kb.nCtus * kb.nRefs);
+    const unsigned grid = (unsigned)(kb.nItems * kb.nCtus * kb.nPairs);
     VAME_TRY(time_begin(c, 1, sBig));
     if (c->prof)
       hipLaunchKernelGGL(affine_me_ctu_prof, dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig, kb);
@@ -265,7 +264,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     KParams kq = kp;
     kq.items = quadFull ? c->dQuad : c->dQuad + c->nQuadFull;
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
-    const unsigned grid = (unsigned)(kq.nItems * kq.nCtus * kq.nRefs);
+    const unsigned grid = (unsigned)(kq.nItems * kq.nCtus * kq.nPairs);
     VAME_TRY(time_begin(c, 0, sQuad));
     if (c->prof)
       hipLaunchKernelGGL(affine_me_quad_prof, dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad, kq);
@@ -385,51 +384,72 @@ int vame_affine_me(vame_ctx* c, const uint16_t* ref, const uint16_t* cur, float 
   VAME_HIP(hipSetDevice(c->device));
   KParams kp;
   memset(&kp, 0, sizeof(kp));
-  fill_common(kp, c, lambda, extra);
-  kp.cur = cur;
-  kp.refs[0] = ref;
-  kp.nRefs = 1;
+  fill_common(kp, c, extra);
+  kp.pair[0].cur = cur;
+  kp.pair[0].ref = ref;
+  kp.pair[0].lambda = lambda;
+  kp.nPairs = 1;
   kp.run2 = nCP == 2;
   kp.run3 = nCP == 3;
   const int mode = align * 2 + (nCP - 2);
-  kp.cost[0][mode] = cost;
-  kp.cpmv[0][mode] = reinterpret_cast<vame_cpmvs_dev*>(cpmvs);
+  kp.pair[0].cost[mode] = cost;
+  kp.pair[0].cpmv[mode] = reinterpret_cast<vame_cpmvs_dev*>(cpmvs);
   kp.prev[align] = reinterpret_cast<const vame_cpmvs_dev*>(prev);
   return launch(c, kp, align == 0, align == 1, align == 0, (hipStream_t)stream);
+}
+
+int vame_affine_me_batch(vame_ctx* c, const vame_poc_job* jobs, int njobs, int mode_mask,
+                         int extra, void* stream) {
+  if (!c || !jobs || njobs < 1) return VAME_E_INVALID;
+  if (!(mode_mask & VAME_MODE_2CP) || (mode_mask & ~3) || extra < 0 || extra > 64)
+    return VAME_E_INVALID;
+  const bool run3 = (mode_mask & VAME_MODE_3CP) != 0;
+  for (int j = 0; j < njobs; j++) {
+    const vame_poc_job& jb = jobs[j];
+    if (!jb.cur || !jb.refs || !jb.out || jb.nrefs < 1) return VAME_E_INVALID;
+    if (jb.nrefs > 4) return VAME_E_UNSUPPORTED;
+    for (int r = 0; r < jb.nrefs; r++) {
+      if (!jb.refs[r]) return VAME_E_INVALID;
+      for (int m = 0; m < 4; m++) {
+        const bool need = (m & 1) ? run3 : true;
+        if (need && (!jb.out->cost[r][m] || !jb.out->cpmvs[r][m])) return VAME_E_INVALID;
+      }
+    }
+  }
+  VAME_HIP(hipSetDevice(c->device));
+  // every (POC, refIdx) pair of the batch, kMaxPairs per launch
+  KParams kp;
+  memset(&kp, 0, sizeof(kp));
+  fill_common(kp, c, extra);
+  kp.run2 = 1;
+  kp.run3 = run3;
+  for (int j = 0; j < njobs; j++) {
+    const vame_poc_job& jb = jobs[j];
+    for (int r = 0; r < jb.nrefs; r++) {
+      PairArgs& pa = kp.pair[kp.nPairs++];
+      pa.cur = jb.cur;
+      pa.ref = jb.refs[r];
+      pa.lambda = jb.lambda;
+      for (int m = 0; m < 4; m++) {
+        pa.cost[m] = jb.out->cost[r][m];
+        pa.cpmv[m] = reinterpret_cast<vame_cpmvs_dev*>(jb.out->cpmvs[r][m]);
+      }
+      const bool last = j == njobs - 1 && r == jb.nrefs - 1;
+      if (kp.nPairs == kMaxPairs || last) {
+        VAME_TRY(launch(c, kp, true, true, true, (hipStream_t)stream));
+        kp.nPairs = 0;
+      }
+    }
+  }
+  return VAME_OK;
 }
 
 int vame_affine_me_poc(vame_ctx* c, const uint16_t* cur, const uint16_t* const* refs, int nrefs,
                        float lambda, int mode_mask, int extra, const vame_poc_result* out,
                        void* stream) {
-  if (!c || !cur || !refs || !out) return VAME_E_INVALID;
-  if (nrefs < 1) return VAME_E_INVALID;
-  if (nrefs > 4) return VAME_E_UNSUPPORTED;
-  if (!(mode_mask & VAME_MODE_2CP) || (mode_mask & ~3) || extra < 0 || extra > 64)
-    return VAME_E_INVALID;
-  const bool run3 = (mode_mask & VAME_MODE_3CP) != 0;
-  for (int r = 0; r < nrefs; r++) {
-    if (!refs[r]) return VAME_E_INVALID;
-    for (int m = 0; m < 4; m++) {
-      const bool need = (m & 1) ? run3 : true;
-      if (need && (!out->cost[r][m] || !out->cpmvs[r][m])) return VAME_E_INVALID;
-    }
-  }
-  VAME_HIP(hipSetDevice(c->device));
-  KParams kp;
-  memset(&kp, 0, sizeof(kp));
-  fill_common(kp, c, lambda, extra);
-  kp.cur = cur;
-  kp.nRefs = nrefs;
-  kp.run2 = 1;
-  kp.run3 = run3;
-  for (int r = 0; r < nrefs; r++) {
-    kp.refs[r] = refs[r];
-    for (int m = 0; m < 4; m++) {
-      kp.cost[r][m] = out->cost[r][m];
-      kp.cpmv[r][m] = reinterpret_cast<vame_cpmvs_dev*>(out->cpmvs[r][m]);
-    }
-  }
-  return launch(c, kp, true, true, true, (hipStream_t)stream);
+  if (!out) return VAME_E_INVALID;
+  const vame_poc_job job{cur, refs, nrefs, lambda, out};
+  return vame_affine_me_batch(c, &job, 1, mode_mask, extra, stream);
 }
 
 int vame_set_prof(vame_ctx* c, int enable) {

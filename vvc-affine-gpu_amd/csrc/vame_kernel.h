@@ -76,16 +76,24 @@ struct Item {
   CuSlot cu[kMaxCu];
 };
 
-struct KParams {
+// One (POC, refIdx) pair of a launch: the reference's kernel arguments for it
+// (affine.cl:11 / :960: frames, lambda, result arrays per PRED).
+struct PairArgs {
   const uint16_t* cur;
-  const uint16_t* refs[4];
-  int64_t* cost[4][4];        // [ref][FULL_2CP, FULL_3CP, HALF_2CP, HALF_3CP]
-  vame_cpmvs_dev* cpmv[4][4];
+  const uint16_t* ref;
+  int64_t* cost[4];           // [FULL_2CP, FULL_3CP, HALF_2CP, HALF_3CP]
+  vame_cpmvs_dev* cpmv[4];
+  float lambda;
+  int32_t pad;
+};
+constexpr int kMaxPairs = 32;  // pairs per launch (kernel-argument table, 2.9 KB)
+
+struct KParams {
+  PairArgs pair[kMaxPairs];
   const vame_cpmvs_dev* prev[2];  // [align]: 3-CP seeds when the 2-CP pass is not run
   const Item* items;
-  int nItems, nCtus, nRefs;
+  int nItems, nCtus, nPairs;
   int W, H, ctusPerRow;
-  float lambda;
   int extra;
   int run2, run3;
 };
@@ -1193,10 +1201,11 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   const int itemIdx = logical % p.nItems;
   const int rest = logical / p.nItems;
   const int ctu = rest % p.nCtus;
-  const int refIdx = rest / p.nCtus;
+  const int pairIdx = rest / p.nCtus;  // (POC, refIdx) pair of this launch
+  const PairArgs& pa = p.pair[pairIdx];
   const Item* it = p.items + itemIdx;
-  const uint16_t* __restrict__ ref = p.refs[refIdx];
-  const uint16_t* __restrict__ cur = p.cur;
+  const uint16_t* __restrict__ ref = pa.ref;
+  const uint16_t* __restrict__ cur = pa.cur;
   const int W = p.W, H = p.H;
   const int ctuX = (ctu % p.ctusPerRow) * kCtu, ctuY = (ctu / p.ctusPerRow) * kCtu;
 
@@ -1417,7 +1426,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         if (myCu >= 0 && local == 7) {
           CuState& st = s_st[myCu];
           if (rate) {
-            const float prod = __fmul_rn(p.lambda, (float)(b + kRuiBits));
+            const float prod = __fmul_rn(pa.lambda, (float)(b + kRuiBits));
             const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
             if (cost < st.bestCost) {
               st.bestCost = cost;
@@ -1556,12 +1565,12 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       const CuSlot cs = s_cu[k];
       const int mode = cs.align * 2 + (ncp - 2);
       const size_t idx = (size_t)ctu * (cs.align ? kHalfCusPerCtu : kFullCusPerCtu) + cs.outOff;
-      p.cost[refIdx][mode][idx] = st.bestCost;
+      pa.cost[mode][idx] = st.bestCost;
       vame_cpmvs_dev o;
       o.ncps = ncp;
       o.ltx = st.best[0]; o.lty = st.best[1]; o.rtx = st.best[2];
       o.rty = st.best[3]; o.lbx = st.best[4]; o.lby = st.best[5];
-      p.cpmv[refIdx][mode][idx] = o;
+      pa.cpmv[mode][idx] = o;
     }
     phase_sync(coop);
     PH_MARK(kPhTail)

@@ -14,7 +14,7 @@ EXPORTS = (
     "vame_cus_per_ctu", "vame_num_groups", "vame_group_geometry", "vame_lambda", "vame_poc_qp",
     "vame_ref_list", "vame_strerror", "vame_last_hip_error", "vame_version", "vame_set_timing",
     "vame_get_timing", "vame_read_frames", "vame_log_remove_old", "vame_log_write_headers",
-    "vame_log_append", "vame_log_file_count", "vame_set_prof",
+    "vame_log_append", "vame_log_file_count", "vame_set_prof", "vame_affine_me_batch",
 )
 
 
@@ -24,6 +24,12 @@ class VameError(RuntimeError):
 
 class PocResult(ctypes.Structure):
     _fields_ = [("cost", (ctypes.c_void_p * 4) * 4), ("cpmvs", (ctypes.c_void_p * 4) * 4)]
+
+
+class PocJob(ctypes.Structure):
+    """vame_poc_job (include/vame.h)."""
+    _fields_ = [("cur", ctypes.c_void_p), ("refs", ctypes.c_void_p), ("nrefs", ctypes.c_int),
+                ("lam", ctypes.c_float), ("out", ctypes.c_void_p)]
 
 
 _lib = None
@@ -41,6 +47,7 @@ def lib():
         L.vame_destroy.restype = None
         L.vame_affine_me.argtypes = [P, P, P, F, I, I, I, P, P, P, P]
         L.vame_affine_me_poc.argtypes = [P, P, P, I, F, I, I, ctypes.POINTER(PocResult), P]
+        L.vame_affine_me_batch.argtypes = [P, ctypes.POINTER(PocJob), I, I, I, P]
         L.vame_num_ctus.argtypes = [I, I]
         L.vame_cus_per_ctu.argtypes = [I]
         L.vame_num_groups.argtypes = [I]

@@ -5,7 +5,9 @@ Mirrors the reference's operator interface for this path:
     affine_gradient_mult_sizes(_HA) built with -DnCP=ncp (affine.cl:11/:960,
     args set at main.cpp:827-840), returning the gBestCost / gBestCpmvs arrays;
   * `Engine.affine_me_poc(cur, refs, lam, ...)` == the whole refIdx loop of one
-    POC (main.cpp:746-966), fused into one pass.
+    POC (main.cpp:746-966), fused into one pass;
+  * `Engine.affine_me_batch([(cur, refs, lam, out), ...])` == several POCs'
+    affine_me_poc calls in shared launches.
 Frames are (H, W) int16/uint16 tensors of 10-bit samples on the engine's device.
 """
 from __future__ import annotations
@@ -14,7 +16,7 @@ import ctypes
 
 import torch
 
-from ._lib import PocResult, check, lib
+from ._lib import PocJob, PocResult, check, lib
 
 CPMV_FIELDS = ("nCPs", "LTx", "LTy", "RTx", "RTy", "LBx", "LBy")
 MODES = ("FULL_2CP", "FULL_3CP", "HALF_2CP", "HALF_3CP")
@@ -98,6 +100,29 @@ class Engine:
                     continue
                 res[(r, name)] = self.alloc_result(m >> 1)
         return res
+
+    def affine_me_batch(self, jobs, modes: int = 3, extra: int = 0):
+        """jobs: [(cur, refs, lam, out)] with out from alloc_poc; one
+        vame_affine_me_batch call (32 (POC, refIdx) pairs per launch)."""
+        keep = []
+        arr = (PocJob * len(jobs))()
+        for j, (cur, refs, lam, out) in enumerate(jobs):
+            cur = self._frame(cur)
+            refs = [self._frame(r) for r in refs]
+            pr = PocResult()
+            for (r, name), (cost, cpmv) in out.items():
+                m = MODES.index(name)
+                pr.cost[r][m] = cost.data_ptr()
+                pr.cpmvs[r][m] = cpmv.data_ptr()
+            ref_ptrs = (ctypes.c_void_p * len(refs))(*[r.data_ptr() for r in refs])
+            keep += [cur, refs, pr, ref_ptrs]
+            arr[j].cur = cur.data_ptr()
+            arr[j].refs = ctypes.cast(ref_ptrs, ctypes.c_void_p)
+            arr[j].nrefs = len(refs)
+            arr[j].lam = float(lam)
+            arr[j].out = ctypes.cast(ctypes.pointer(pr), ctypes.c_void_p)
+        check(lib().vame_affine_me_batch(self._h, arr, len(jobs), modes, extra, self._stream()))
+        return [job[3] for job in jobs]
 
     def affine_me_poc(self, cur, refs, lam: float, modes: int = 3, extra: int = 0, out=None):
         """modes: 1 = 2-CP only, 3 = 2-CP then 3-CP.  Returns {(refIdx, MODE): (cost, cpmv)}."""
