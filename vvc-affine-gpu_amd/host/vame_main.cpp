@@ -243,6 +243,7 @@ void test_references(int n_frames, int qp) {
 
 // ------------------------------------------------------------ results
 constexpr int kFull = 201, kHalf = 284;
+constexpr int kBatchPocs = 4;  // POCs per vame_affine_me_batch call (<= 16 pairs)
 
 struct Layout {  // one POC's results: [ref][pred] cost block, then cpmvs block
   size_t off_cost[4][4], off_cp[4][4], bytes;
@@ -262,6 +263,7 @@ struct Layout {  // one POC's results: [ref][pred] cost block, then cpmvs block
 
 struct Slab {
   char* host = nullptr;  // pinned
+  int owner = 0;         // the worker whose pool it returns to
   int poc = 0, nrefs = 0;
   float pred_ns[4] = {0, 0, 0, 0};  // per-launch mode kernel times
   float fused_ns = 0;
@@ -270,14 +272,16 @@ struct Slab {
 struct Shared {
   std::mutex mu;
   std::condition_variable cv;
-  std::vector<Slab*> pool;
+  // one pool per worker: a worker running ahead of the in-order writer can only
+  // exhaust its own slabs, never the ones the writer is waiting for
+  std::vector<std::vector<Slab*>> pools;
   std::map<int, Slab*> done;
   std::string error;
   bool failed = false;
 };
 
 struct Job {
-  int device, W, H, nCtus, qp, extra, mode_mask;
+  int worker, device, W, H, nCtus, qp, extra, mode_mask;
   bool per_launch;
   bool prof;
   std::vector<int> pocs;
@@ -339,9 +343,13 @@ void gpu_worker(Job J) {
                   "upload recon");
       }
   }
-  char* dres = nullptr;
-  GPU_CHECK(hipMalloc(&dres, J.L->bytes), "hipMalloc results");
-  // two slots: POC k+1 is enqueued before the host waits for POC k's copy
+  // POCs run in batches: the fused path hands a batch of up to kBatchPocs POCs
+  // (<= 32 (POC, refIdx) pairs) to one vame_affine_me_batch call, so they share
+  // launches; --per-launch keeps the reference's one launch per (refIdx, PRED)
+  const int B = J.per_launch ? 1 : kBatchPocs;
+  char* dres = nullptr;  // two batch slots of B POC layouts each
+  GPU_CHECK(hipMalloc(&dres, 2 * (size_t)B * J.L->bytes), "hipMalloc results");
+  // two slots: batch k+1 is enqueued before the host waits for batch k's copies
   hipEvent_t e0[2], e1[2], copied[2];
   for (int i = 0; i < 2; i++) {
     GPU_CHECK(hipEventCreate(&e0[i]), "hipEventCreate");
@@ -349,14 +357,15 @@ void gpu_worker(Job J) {
     GPU_CHECK(hipEventCreateWithFlags(&copied[i], hipEventDisableTiming), "hipEventCreate");
   }
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evs[2];  // per-launch timing events
-  Slab* pending = nullptr;
+  std::vector<Slab*> pending;
   int pslot = 0;
 
-  // waits for a slot's copy, collects its kernel times, hands the slab to the writer
-  auto finish = [&](Slab* s, int slot) -> bool {
+  // waits for a slot's copies, collects its kernel times, hands the slabs to the writer
+  auto finish = [&](std::vector<Slab*>& batch, int slot) -> bool {
     if (hipEventSynchronize(copied[slot]) != hipSuccess) return false;
     float ms = 0;
     if (J.per_launch) {
+      Slab* s = batch[0];
       for (int r = 0; r < s->nrefs; r++)
         for (int m = 0; m < 4; m++) {
           if ((m & 1) && !(J.mode_mask & VAME_MODE_3CP)) continue;
@@ -366,34 +375,47 @@ void gpu_worker(Job J) {
         }
     } else {
       if (hipEventElapsedTime(&ms, e0[slot], e1[slot]) != hipSuccess) return false;
-      s->fused_ns = ms * 1e6f;
+      batch[0]->fused_ns = ms * 1e6f;  // the batch's kernel time, reported once
     }
     std::lock_guard<std::mutex> g(S->mu);
-    S->done[s->poc] = s;
+    for (Slab* s : batch) S->done[s->poc] = s;
     S->cv.notify_all();
     return true;
   };
 
   int k = 0;
-  for (int p : J.pocs) {
+  for (size_t i0 = 0; i0 < J.pocs.size();) {
     const int slot = k++ & 1;
-    Slab* slab = nullptr;
-    {
-      std::unique_lock<std::mutex> g(S->mu);
-      S->cv.wait(g, [&] { return S->failed || !S->pool.empty(); });
-      if (S->failed) break;
-      slab = S->pool.back();
-      S->pool.pop_back();
+    std::vector<Slab*> batch;
+    int pairs = 0;
+    while (i0 < J.pocs.size() && (int)batch.size() < B) {
+      const int p = J.pocs[i0];
+      const int n = std::min(4, p);
+      if (!batch.empty() && pairs + n > 32) break;
+      Slab* slab = nullptr;
+      {
+        std::unique_lock<std::mutex> g(S->mu);
+        auto& pool = S->pools[J.worker];
+        S->cv.wait(g, [&] { return S->failed || !pool.empty(); });
+        if (S->failed) return;
+        slab = pool.back();
+        pool.pop_back();
+      }
+      slab->poc = p;
+      slab->nrefs = n;
+      batch.push_back(slab);
+      pairs += n;
+      i0++;
     }
-    int refs[4];
-    const int nrefs = vame_ref_list(p, refs);
-    slab->poc = p;
-    slab->nrefs = nrefs;
-    const float lambda = vame_lambda(J.qp, p);
-    auto dcost = [&](int r, int m) { return (int64_t*)(dres + J.L->off_cost[r][m]); };
-    auto dcp = [&](int r, int m) { return (vame_cpmvs*)(dres + J.L->off_cp[r][m]); };
+    auto base = [&](int j) { return dres + ((size_t)slot * B + j) * J.L->bytes; };
     if (J.per_launch) {
       // main.cpp:754-966: per refIdx, FULL_2CP, FULL_3CP, HALF_2CP, HALF_3CP
+      const int p = batch[0]->poc;
+      int refs[4];
+      const int nrefs = vame_ref_list(p, refs);
+      const float lambda = vame_lambda(J.qp, p);
+      auto dcost = [&](int r, int m) { return (int64_t*)(base(0) + J.L->off_cost[r][m]); };
+      auto dcp = [&](int r, int m) { return (vame_cpmvs*)(base(0) + J.L->off_cp[r][m]); };
       while (evs[slot].size() < (size_t)nrefs * 4) {
         std::pair<hipEvent_t, hipEvent_t> e;
         GPU_CHECK(hipEventCreate(&e.first), "hipEventCreate");
@@ -412,33 +434,42 @@ void gpu_worker(Job J) {
           GPU_CHECK(hipEventRecord(e.second, st), "hipEventRecord");
         }
     } else {
-      vame_poc_result out;
-      memset(&out, 0, sizeof out);
-      const uint16_t* rp[4];
-      for (int r = 0; r < nrefs; r++) {
-        rp[r] = drecon[refs[r]];
-        for (int m = 0; m < 4; m++) {
-          if ((m & 1) && !(J.mode_mask & VAME_MODE_3CP)) continue;
-          out.cost[r][m] = dcost(r, m);
-          out.cpmvs[r][m] = dcp(r, m);
+      vame_poc_result out[kBatchPocs];
+      const uint16_t* rp[kBatchPocs][4];
+      vame_poc_job jobs[kBatchPocs];
+      for (size_t j = 0; j < batch.size(); j++) {
+        const int p = batch[j]->poc;
+        int refs[4];
+        const int nrefs = vame_ref_list(p, refs);
+        memset(&out[j], 0, sizeof out[j]);
+        for (int r = 0; r < nrefs; r++) {
+          rp[j][r] = drecon[refs[r]];
+          for (int m = 0; m < 4; m++) {
+            if ((m & 1) && !(J.mode_mask & VAME_MODE_3CP)) continue;
+            out[j].cost[r][m] = (int64_t*)(base((int)j) + J.L->off_cost[r][m]);
+            out[j].cpmvs[r][m] = (vame_cpmvs*)(base((int)j) + J.L->off_cp[r][m]);
+          }
         }
+        jobs[j] = vame_poc_job{dorig[p], rp[j], nrefs, vame_lambda(J.qp, p), &out[j]};
       }
       GPU_CHECK(hipEventRecord(e0[slot], st), "hipEventRecord");
-      VAME_CHECK(vame_affine_me_poc(ctx, dorig[p], rp, nrefs, lambda, J.mode_mask, J.extra, &out, st),
-                 "vame_affine_me_poc");
+      VAME_CHECK(vame_affine_me_batch(ctx, jobs, (int)batch.size(), J.mode_mask, J.extra, st),
+                 "vame_affine_me_batch");
       GPU_CHECK(hipEventRecord(e1[slot], st), "hipEventRecord");
     }
-    // stream order: this POC's kernels run after the previous POC's copy read dres
-    GPU_CHECK(hipMemcpyAsync(slab->host, dres, J.L->bytes, hipMemcpyDeviceToHost, st), "D2H");
+    // stream order: this batch's kernels run after the previous batch's copies read its slot
+    for (size_t j = 0; j < batch.size(); j++)
+      GPU_CHECK(hipMemcpyAsync(batch[j]->host, base((int)j), J.L->bytes, hipMemcpyDeviceToHost, st),
+                "D2H");
     GPU_CHECK(hipEventRecord(copied[slot], st), "hipEventRecord");
-    if (pending && !finish(pending, pslot)) {
+    if (!pending.empty() && !finish(pending, pslot)) {
       fail(S, "waiting for results failed");
       return;
     }
-    pending = slab;
+    pending = batch;
     pslot = slot;
   }
-  if (pending && !finish(pending, pslot)) {
+  if (!pending.empty() && !finish(pending, pslot)) {
     fail(S, "waiting for results failed");
     return;
   }
@@ -589,14 +620,18 @@ int main(int argc, char** argv) {
   print_timestamp("START ALLOCATE MEMORY");
   const Layout L(nCtus);
   Shared S;
-  const int nslabs = std::max(4, 3 * ngpu);
-  std::vector<Slab> slabs(nslabs);
-  for (auto& s : slabs) {
+  // per device: two batches in flight plus two POCs' worth for the writer
+  const int per_worker = per_launch ? 3 : 2 * kBatchPocs + 2;
+  std::vector<Slab> slabs((size_t)per_worker * ngpu);
+  S.pools.resize(ngpu);
+  for (size_t i = 0; i < slabs.size(); i++) {
+    Slab& s = slabs[i];
     if (hipHostMalloc((void**)&s.host, L.bytes, hipHostMallocDefault) != hipSuccess) {
       printf("  [!] ERROR: pinned host allocation of %zu bytes failed\n", L.bytes);
       return 1;
     }
-    S.pool.push_back(&s);
+    s.owner = (int)(i / per_worker);
+    S.pools[s.owner].push_back(&s);
   }
   std::vector<Job> jobs(ngpu);
   {
@@ -618,6 +653,7 @@ int main(int argc, char** argv) {
   std::vector<std::thread> workers;
   for (int g = 0; g < ngpu; g++) {
     Job& j = jobs[g];
+    j.worker = g;
     j.device = devices[g];
     j.W = W;
     j.H = H;
@@ -682,7 +718,7 @@ int main(int argc, char** argv) {
     memset(s->pred_ns, 0, sizeof s->pred_ns);
     s->fused_ns = 0;
     std::lock_guard<std::mutex> g(S.mu);
-    S.pool.push_back(s);
+    S.pools[s->owner].push_back(s);
     S.cv.notify_all();
   }
   if (!ok) {
