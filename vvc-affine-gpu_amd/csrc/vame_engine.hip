@@ -15,7 +15,7 @@
 #include "vame_kernel.h"
 
 #ifndef VAME_BIG_STREAM
-#define VAME_BIG_STREAM 0
+#define VAME_BIG_STREAM 1
 #endif
 
 using namespace vame;
@@ -236,7 +236,11 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
   // 128-class items (big LDS, 1 workgroup per CU) and quadrant items run on
   // two streams so they overlap; VAME_BIG_STREAM picks which one the 128-class
   // kernel is issued on (0: side stream, after an event; 1: caller's stream,
-  // first, with the quadrant kernel on the side stream).
+  // first, with the quadrant kernel on the side stream).  A 128-class
+  // workgroup needs a whole CU (16 waves, 92 KB LDS): issued first, its
+  // workgroups take CUs before the quadrant ones fill them, and the small
+  // quadrant workgroups, not the long 128-class ones, make the tail
+  // (batched c2 step 1.32 -> 1.245 ms).
   if (VAME_ABLATE & 16) bigItems = false;  // timing-only builds
   if (VAME_ABLATE & 32) quadFull = quadHalf = false;
   const bool fork = bigItems && (quadFull || quadHalf);
