@@ -119,6 +119,9 @@ struct KParams {
 #ifndef VAME_PRIO
 #define VAME_PRIO 3
 #endif
+#ifndef VAME_ORDER
+#define VAME_ORDER 3
+#endif
 #ifndef VAME_WAVES
 #define VAME_WAVES 4
 #endif
@@ -1197,9 +1200,18 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   // give each XCD a contiguous run of logical work (same CTUs -> L2 reuse).
   const int nb = gridDim.x, b = blockIdx.x;
   const int q8 = nb >> 3, r8 = nb & 7, xcd = b & 7;
-  const int logical = xcd * q8 + min(xcd, r8) + (b >> 3);
-  const int itemIdx = logical % p.nItems;
-  const int rest = logical / p.nItems;
+  int logical = xcd * q8 + min(xcd, r8) + (b >> 3);
+  int itemIdx = logical % p.nItems;
+  int rest = logical / p.nItems;
+  // Item-major dispatch order (VAME_ORDER bit 0: 128-class kernel, bit 1:
+  // quadrant kernel): all (ctu, pair) blocks of template item 0 first, then
+  // item 1, ...; the host lists the costlier items first, so the tail is made of
+  // short workgroups (blocks b, b+8, ... still spread over the XCDs).
+  if ((VAME_ORDER & (REGION == 128 ? 1 : 2)) != 0) {
+    const int per = nb / p.nItems;  // (ctu, pair) combinations
+    itemIdx = b / per;
+    rest = b % per;
+  }
   const int ctu = rest % p.nCtus;
   const int pairIdx = rest / p.nCtus;  // (POC, refIdx) pair of this launch
   const PairArgs& pa = p.pair[pairIdx];
