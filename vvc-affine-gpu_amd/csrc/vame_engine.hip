@@ -14,9 +14,6 @@
 #include "../../include/vame.h"
 #include "vame_kernel.h"
 
-#ifndef VAME_CUMASK
-#define VAME_CUMASK 0
-#endif
 #ifndef VAME_BIG_STREAM
 #define VAME_BIG_STREAM 1
 #endif
@@ -46,11 +43,6 @@ struct vame_ctx {
   Item* dBig = nullptr;
   int nQuadFull = 0, nQuadHalf = 0, nBig = 0;
   hipStream_t side = nullptr;   // second stream: 128-class items run beside the quadrant items
-  // VAME_CUMASK > 0: the two kernels on CU-masked streams of their own (the
-  // 128-class one on VAME_CUMASK CUs per XCD), forked from / joined into the
-  // caller's stream
-  hipStream_t mBig = nullptr, mQuad = nullptr;
-  hipEvent_t evJoin2 = nullptr;
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   // optional per-kernel timing: (start, end) event pairs per kernel class
   bool timing = false;
@@ -252,15 +244,8 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
   if (VAME_ABLATE & 16) bigItems = false;  // timing-only builds
   if (VAME_ABLATE & 32) quadFull = quadHalf = false;
   const bool fork = bigItems && (quadFull || quadHalf);
-  const bool masked = fork && c->mBig;
   hipStream_t sBig = stream, sQuad = stream;
-  if (masked) {
-    VAME_HIP(hipEventRecord(c->evFork, stream));
-    VAME_HIP(hipStreamWaitEvent(c->mBig, c->evFork, 0));
-    VAME_HIP(hipStreamWaitEvent(c->mQuad, c->evFork, 0));
-    sBig = c->mBig;
-    sQuad = c->mQuad;
-  } else if (fork) {
+  if (fork) {
     VAME_HIP(hipEventRecord(c->evFork, stream));
     VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
     if (VAME_BIG_STREAM) sQuad = c->side; else sBig = c->side;
@@ -295,12 +280,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
   };
   if (bigItems) VAME_TRY(big());
   if (quadFull || quadHalf) VAME_TRY(quad());
-  if (masked) {
-    VAME_HIP(hipEventRecord(c->evJoin, c->mBig));
-    VAME_HIP(hipEventRecord(c->evJoin2, c->mQuad));
-    VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
-    VAME_HIP(hipStreamWaitEvent(stream, c->evJoin2, 0));
-  } else if (fork) {
+  if (fork) {
     VAME_HIP(hipEventRecord(c->evJoin, c->side));
     VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
   }
@@ -373,24 +353,6 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin2, hipEventDisableTiming);
-  if (e == hipSuccess && VAME_CUMASK > 0) {
-    hipDeviceProp_t prop;
-    e = hipGetDeviceProperties(&prop, device);
-    if (e == hipSuccess && prop.multiProcessorCount == 256) {
-      // CU i = 32a + 8b + c: the 128-class stream gets b == 0 and
-      // (c - a) mod 8 < VAME_CUMASK -- VAME_CUMASK CUs of every XCD whether
-      // the mask maps CUs to XCDs in blocks of 32 (a) or round-robin (c)
-      uint32_t mb[8] = {0}, mq[8] = {0};
-      for (int i = 0; i < 256; i++) {
-        const int a = i >> 5, b = (i >> 3) & 3, cc = i & 7;
-        const bool big = b == 0 && ((cc - a) & 7) < VAME_CUMASK;
-        (big ? mb : mq)[i >> 5] |= 1u << (i & 31);
-      }
-      e = hipExtStreamCreateWithCUMask(&c->mBig, 8, mb);
-      if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&c->mQuad, 8, mq);
-    }
-  }
   if (e != hipSuccess) {
     snprintf(g_hip_err, sizeof(g_hip_err), "%s", hipGetErrorString(e));
     vame_destroy(c);
@@ -408,9 +370,6 @@ void vame_destroy(vame_ctx* c) {
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->evFork) (void)hipEventDestroy(c->evFork);
   if (c->evJoin) (void)hipEventDestroy(c->evJoin);
-  if (c->evJoin2) (void)hipEventDestroy(c->evJoin2);
-  if (c->mBig) (void)hipStreamDestroy(c->mBig);
-  if (c->mQuad) (void)hipStreamDestroy(c->mQuad);
   for (int k = 0; k < 2; k++)
     for (auto& e : c->ev[k]) {
       (void)hipEventDestroy(e.first);
