@@ -161,7 +161,7 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& quadFull,
     if (w == 128 || h == 128) {
       std::vector<CuDesc> c;
       for (int k = 0; k < n; k++) c.push_back({(k % cols) * w, (k / cols) * h, w, h, 0, kFullStride[g] + k});
-      big.push_back(make_coop_item(0, 0, c, Cfg<128>::THREADS));
+      if (!((VAME_ABLATE & 256) && w != h)) big.push_back(make_coop_item(0, 0, c, Cfg<128>::THREADS));
     }
   }
   for (int q = 0; q < 4; q++) {

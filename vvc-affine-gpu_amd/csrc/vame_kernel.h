@@ -101,7 +101,8 @@ struct KParams {
 // VAME_ABLATE (timing-only builds, results are wrong): bit 0 skip the solve,
 // bit 1 skip the gradient math, bit 2 skip the reductions of the equations,
 // bit 3 skip the prediction math, bit 4 skip the 128-class launch, bit 5 skip
-// the quadrant launch.
+// the quadrant launch, bit 8 (host) 128-class templates without the 128x64 /
+// 64x128 items.
 #ifndef VAME_ABLATE
 #define VAME_ABLATE 0
 #endif
