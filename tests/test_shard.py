@@ -81,11 +81,17 @@ def test_poc_shard_covers_and_balances():
 
 def test_pack_unpack_roundtrip():
     g = torch.Generator().manual_seed(1)
-    res = [{(r, m): (torch.randint(-2**40, 2**40, (n,), dtype=torch.int64, generator=g),
-                     torch.randint(-2**20, 2**20, (n, 7), dtype=torch.int32, generator=g))
-            for r in range(nr) for m, n in (("FULL_2CP", 10), ("HALF_2CP", 12))}
+    def rec(n, ncp):  # ABI records as the kernels write them: nCPs, 2-CP LB = 0, cost < 2^31
+        cp = torch.randint(-2**17, 2**17, (n, 7), dtype=torch.int32, generator=g)
+        cp[:, 0] = ncp
+        if ncp == 2:
+            cp[:, 5:] = 0
+        return torch.randint(0, 2**31, (n,), dtype=torch.int64, generator=g), cp
+    res = [{(r, m): rec(n, 3 if m.endswith("3CP") else 2)
+            for r in range(nr) for m, n in (("FULL_2CP", 10), ("FULL_3CP", 10), ("HALF_2CP", 12),
+                                            ("HALF_3CP", 12))}
            for nr in (1, 3)]
-    lay = [(1, 1, (10, 12)), (3, 1, (10, 12))]
+    lay = [(1, 3, (10, 12)), (3, 3, (10, 12))]
     flat = shard.pack(res, shard.slab_words(lay) + 5)
     back = shard.unpack(flat, lay)
     for a, b in zip(res, back):

@@ -8,8 +8,13 @@ data path; the only exchange is the decision-log gather at the end (one
 all_gather of equal-size padded int32 slabs, RCCL over xGMI on the GPU box,
 gloo in the CPU tests).
 
-Decision records travel as int32 words: per (POC, ref, mode) the int64 costs
-(2 words each) followed by the [n, 7] Cpmvs words (typedef.h Cpmvs layout).
+Decision records travel compacted, as int32 words: per (POC, ref, mode) the
+costs (one word each) followed by the mode's CPMV components ([n, 4] for
+2 CP: LT, RT -- LB is (0, 0) and nCPs is implied; [n, 6] for 3 CP), i.e. 20 /
+28 bytes per candidate CU instead of the 36 of the ABI records.  A cost always
+fits int32: the SATD of a 128x128 CU is below 1024 * 2^17 < 2^28, the rate term
+is a few thousand, and the initial best is MAX_LONG as the reference's OpenCL
+evaluates it, 2^30.  `unpack` rebuilds the ABI records exactly.
 """
 from __future__ import annotations
 
@@ -51,16 +56,20 @@ def result_keys(nrefs: int, modes: int):
     return keys
 
 
+def ncp_of(mode: str) -> int:
+    return 3 if mode.endswith("3CP") else 2
+
+
 def pack(results: list[dict], words: int | None = None, device=None) -> torch.Tensor:
     """Concatenate the results of several POCs ({(ref, MODE): (cost int64[n],
-    cpmv int32[n, 7])}, in POC order) into one int32 slab, zero padded to
-    `words`."""
+    cpmv int32[n, 7])}, in POC order) into one int32 slab of compact records,
+    zero padded to `words`."""
     parts = []
     for res in results:
         for key in sorted(res, key=lambda k: (k[0], MODES.index(k[1]))):
             cost, cpmv = res[key]
-            parts.append(cost.reshape(-1).contiguous().view(torch.int32))
-            parts.append(cpmv.reshape(-1).to(torch.int32))
+            parts.append(cost.reshape(-1).to(torch.int32))
+            parts.append(cpmv.reshape(-1, 7)[:, 1:1 + 2 * ncp_of(key[1])].reshape(-1).to(torch.int32))
     flat = torch.cat(parts) if parts else torch.empty(0, dtype=torch.int32, device=device)
     if words is not None:
         if flat.numel() > words:
@@ -77,10 +86,13 @@ def unpack(flat: torch.Tensor, layout: list[tuple[int, int, int]]) -> list[dict]
         res = {}
         for key in result_keys(nrefs, modes):
             n = n_half if key[1].startswith("HALF") else n_full
-            cost = flat[ofs:ofs + 2 * n].contiguous().view(torch.int64)
-            ofs += 2 * n
-            cpmv = flat[ofs:ofs + 7 * n].view(n, 7)
-            ofs += 7 * n
+            ncp = ncp_of(key[1])
+            cost = flat[ofs:ofs + n].to(torch.int64)
+            ofs += n
+            cpmv = flat.new_zeros(n, 7)
+            cpmv[:, 0] = ncp
+            cpmv[:, 1:1 + 2 * ncp] = flat[ofs:ofs + 2 * ncp * n].view(n, 2 * ncp)
+            ofs += 2 * ncp * n
             res[key] = (cost, cpmv)
         out.append(res)
     return out
@@ -90,7 +102,7 @@ def slab_words(layout: list[tuple[int, int, int]]) -> int:
     w = 0
     for nrefs, modes, (n_full, n_half) in layout:
         for key in result_keys(nrefs, modes):
-            w += 9 * (n_half if key[1].startswith("HALF") else n_full)
+            w += (1 + 2 * ncp_of(key[1])) * (n_half if key[1].startswith("HALF") else n_full)
     return w
 
 
