@@ -14,6 +14,9 @@
 #include "../../include/vame.h"
 #include "vame_kernel.h"
 
+#ifndef VAME_PAD8
+#define VAME_PAD8 1
+#endif
 #ifndef VAME_BIG_STREAM
 #define VAME_BIG_STREAM 1
 #endif
@@ -231,6 +234,10 @@ int time_end(vame_ctx* c, int cls, hipStream_t s) {
     if (rc_) return rc_;   \
   } while (0)
 
+// (ctu, pair) blocks per template item, padded to a multiple of 8 (one per
+// XCD) under VAME_PAD8 so every item of a CTU lands on the same XCD
+int combos(int n) { return VAME_PAD8 ? (n + 7) / 8 * 8 : n; }
+
 int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
            hipStream_t stream) {
   // 128-class items (big LDS, 1 workgroup per CU) and quadrant items run on
@@ -254,7 +261,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     KParams kb = kp;
     kb.items = c->dBig;
     kb.nItems = c->nBig;
-    const unsigned grid = (unsigned)(kb.nItems * kb.nCtus * kb.nPairs);
+    const unsigned grid = (unsigned)(kb.nItems * combos(kb.nCtus * kb.nPairs));
     VAME_TRY(time_begin(c, 1, sBig));
     if (c->prof)
       hipLaunchKernelGGL(affine_me_ctu_prof, dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig, kb);
@@ -268,7 +275,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     KParams kq = kp;
     kq.items = quadFull ? c->dQuad : c->dQuad + c->nQuadFull;
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
-    const unsigned grid = (unsigned)(kq.nItems * kq.nCtus * kq.nPairs);
+    const unsigned grid = (unsigned)(kq.nItems * combos(kq.nCtus * kq.nPairs));
     VAME_TRY(time_begin(c, 0, sQuad));
     if (c->prof)
       hipLaunchKernelGGL(affine_me_quad_prof, dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad, kq);

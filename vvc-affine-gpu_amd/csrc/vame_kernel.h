@@ -1209,9 +1209,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   // item 1, ...; the host lists the costlier items first, so the tail is made of
   // short workgroups (blocks b, b+8, ... still spread over the XCDs).
   if ((VAME_ORDER & (REGION == 128 ? 1 : 2)) != 0) {
-    const int per = nb / p.nItems;  // (ctu, pair) combinations
+    // the host pads the (ctu, pair) combinations of an item to a multiple of
+    // 8 (VAME_PAD8), so combination j runs on XCD j % 8 for every item: the
+    // items of one CTU re-read its reference tile from the same L2
+    const int per = nb / p.nItems;
     itemIdx = b / per;
     rest = b % per;
+    if (rest >= p.nCtus * p.nPairs) return;  // padding block (uniform, before any barrier)
   }
   const int ctu = rest % p.nCtus;
   const int pairIdx = rest / p.nCtus;  // (POC, refIdx) pair of this launch
@@ -1328,8 +1332,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 
     // ---- per-CU initial CPMVs (2 CP: zero; 3 CP: derived from the 2-CP winner)
     if (lane < nCuW) {
-      int k = cuB + lane;
+      int k = __lane_id();  // == lane, recomputed: not a spilled loop-carried copy
       opaque(k);
+      k += cuB;
       const CuSlot cs = s_cu[k];
       CuState& st = s_st[k];
       const int cx = ctuX + cs.x, cy = ctuY + cs.y;
@@ -1356,12 +1361,18 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         clip_mv(lbx, lby, cx, cy, W, H);
         c[0] = prev[0]; c[1] = prev[1]; c[2] = prev[2]; c[3] = prev[3]; c[4] = lbx; c[5] = lby;
       }
+      // fresh constants (opaque): as loop-carried values the compiler kept
+      // them in spill slots, whose scratch traffic reached HBM
+      int never = (int)0x80000000;  // outside the clamped CPMV range: never matches
+      int costInit = (int)kCostInit;
+      opaque(never);
+      opaque(costInit);
       for (int i = 0; i < 6; i++) {
         st.cur[i] = c[i];
-        st.prev[i] = (int)0x80000000;  // outside the clamped CPMV range: never matches
+        st.prev[i] = never;
         st.best[i] = c[i];
       }
-      st.bestCost = kCostInit;
+      st.bestCost = (long long)costInit;
       st.satd = 0;
       st.inframe = (cx + (1 << cs.lw) <= W) && (cy + (1 << cs.lh) <= H);
       st.live = st.inframe;
@@ -1572,8 +1583,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     }
     // =============== results (affine.cl:928-957) ===============
     if (lane < nCuW) {
-      int k = cuB + lane;
+      int k = __lane_id();  // == lane, recomputed: not a spilled loop-carried copy
       opaque(k);
+      k += cuB;
       const CuState& st = s_st[k];
       const CuSlot cs = s_cu[k];
       const int mode = cs.align * 2 + (ncp - 2);
