@@ -17,6 +17,12 @@
 #ifndef VAME_PAD8
 #define VAME_PAD8 1
 #endif
+#ifndef VAME_TFLAGS
+#define VAME_TFLAGS hipEventDisableSystemFence
+#endif
+#ifndef VAME_JFLAGS
+#define VAME_JFLAGS 0
+#endif
 #ifndef VAME_BIG_STREAM
 #define VAME_BIG_STREAM 1
 #endif
@@ -214,8 +220,10 @@ int time_begin(vame_ctx* c, int cls, hipStream_t s) {
   auto& v = c->ev[cls];
   if (c->evUsed[cls] == v.size()) {
     std::pair<hipEvent_t, hipEvent_t> e;
-    VAME_HIP(hipEventCreate(&e.first));
-    VAME_HIP(hipEventCreate(&e.second));
+    // timing-only events: no system-scope fence (no cache writeback /
+    // invalidation between the kernels they bracket)
+    VAME_HIP(hipEventCreateWithFlags(&e.first, VAME_TFLAGS));
+    VAME_HIP(hipEventCreateWithFlags(&e.second, VAME_TFLAGS));
     v.push_back(e);
   }
   VAME_HIP(hipEventRecord(v[c->evUsed[cls]].first, s));
@@ -358,8 +366,8 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (e == hipSuccess) e = hipMemcpy(c->dQuad, quad.data(), quad.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->dBig, big.data(), big.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming | VAME_JFLAGS);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming | VAME_JFLAGS);
   if (e != hipSuccess) {
     snprintf(g_hip_err, sizeof(g_hip_err), "%s", hipGetErrorString(e));
     vame_destroy(c);
