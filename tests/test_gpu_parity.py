@@ -237,3 +237,23 @@ def test_batch_equals_per_poc(engines):
     for name, key in MODES.items():
         hc, hp = host(outs[11][(0, name)])
         np.testing.assert_array_equal(hc, want[key][0], err_msg=name)
+
+
+@pytest.mark.parametrize("d", [(2, -3), (-4, 1)])
+def test_property_translation_1080p(engines, d):
+    """Full BASELINE size (1920x1080): a frame shifted by an integer d is found
+    as that translation (LT == RT == -16 d) by >= 75 % of the interior 32x32
+    and 64x64 FULL CUs (SURVEY.md §8c property test; the oracle agrees at
+    416x240, test_oracle.py::test_property_integer_translation)."""
+    from vame import synth
+    from test_oracle import translation_ok_fraction
+    W, H = 1920, 1080
+    ref = synth.synth_frame(W, H, 0, 0x1234)
+    cur = np.roll(np.roll(ref, d[1], axis=0), d[0], axis=1)
+    eng = engines(W, H)
+    c, p = host(eng.affine_me(dev(ref), dev(cur), 40.0, 0, 2))
+    cp = np.zeros(len(c), O.CPMVS_DTYPE)
+    for i, f in enumerate(O.CPMVS_DTYPE.names):
+        cp[f] = p[:, i]
+    frac, n = translation_ok_fraction(cp, W, H, d)
+    assert n > 1000 and frac >= 0.75, (frac, n)

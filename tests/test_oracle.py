@@ -172,3 +172,39 @@ def test_prof_matches_reference_functions():
         else:
             out = O.predict_4x4_prof(frame, 3, 3, q[9], q[10], dh, dv)
         np.testing.assert_array_equal(out, z["pred"][g], err_msg=f"case {g}")
+
+
+def translation_ok_fraction(cp, W, H, d, groups=(3, 6), cus_per_ctu=201):
+    """Fraction of interior FULL CUs of the given groups whose 2-CP winner is the
+    pure translation (LT == RT == -16 d, 1/16 pel) -- the survey's property
+    test: a frame shifted by an integer d is found as that
+    motion by the gradient refinement."""
+    geo = O.group_geometry(0)
+    ctus_per_row = (W + 127) // 128
+    n_ctus = O.lib().vame_oracle_num_ctus(W, H)
+    want = np.array([-16 * d[0], -16 * d[1]])
+    hit = tot = 0
+    for g in groups:
+        w, h, xs, ys, stride = geo[g]
+        for ctu in range(n_ctus):
+            x0, y0 = (ctu % ctus_per_row) * 128, (ctu // ctus_per_row) * 128
+            for k in range(len(xs)):
+                x, y = x0 + xs[k], y0 + ys[k]
+                if x < 8 or y < 8 or x + w > W - 8 or y + h > H - 8:
+                    continue
+                c = cp[ctu * cus_per_ctu + stride + k]
+                tot += 1
+                hit += int(abs(c["LTx"] - want[0]) <= 0 and abs(c["LTy"] - want[1]) <= 0
+                           and abs(c["RTx"] - want[0]) <= 0 and abs(c["RTy"] - want[1]) <= 0)
+    return hit / max(tot, 1), tot
+
+
+@pytest.mark.parametrize("d", [(3, -2), (-5, 1), (0, 4)])
+def test_property_integer_translation(d):
+    from vame import synth
+    W, H = 416, 240
+    ref = synth.synth_frame(W, H, 0, 0x1234)
+    cur = np.roll(np.roll(ref, d[1], axis=0), d[0], axis=1)
+    cost, cp = O.affine_me(ref, cur, 40.0, 0, 2)
+    frac, n = translation_ok_fraction(cp, W, H, d)
+    assert n > 50 and frac >= 0.75, (frac, n)

@@ -113,3 +113,55 @@ def test_two_rank_gather_equals_single_process(tmp_path):
         for (r, m), (c, p) in want.items():
             gc, gp = g[f"{r}:{m}"]
             assert torch.equal(gc, c) and torch.equal(gp, p), (poc, r, m)
+
+
+def gpu_worker(rank, world, port, outdir):
+    """One rank of the GPU frame-shard run: its POC block through the HIP engine
+    (vame_affine_me_batch on cuda:0 -- both ranks share the test box's one GPU),
+    compact records all_gathered over gloo."""
+    from vame.engine import Engine
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    orig, recon = synth.synth_sequence(W, H, NF, QP, seed=7)
+    dev = torch.device("cuda", 0)
+    eng = Engine(W, H, 0)
+    mine = shard.poc_shard(NF, world, rank)
+    jobs = []
+    for p in mine:
+        refs = [torch.from_numpy(recon[r].view(np.int16)).to(dev) for r in ref_list(p)]
+        jobs.append((torch.from_numpy(orig[p - 1].view(np.int16)).to(dev), refs,
+                     lambda_for_poc(QP, p), eng.alloc_poc(len(refs), 1)))
+    outs = eng.affine_me_batch(jobs, 1, 0)
+    torch.cuda.synchronize()
+    words = max(shard.slab_words(layout(shard.poc_shard(NF, world, r))) for r in range(world))
+    slabs = shard.gather(shard.pack(outs, words, dev).cpu(), world)
+    if rank == 0:
+        allres = []
+        for r in range(world):
+            allres += shard.unpack(slabs[r], layout(shard.poc_shard(NF, world, r)))
+        torch.save([{f"{k[0]}:{k[1]}": (c.clone(), p.clone()) for k, (c, p) in res.items()}
+                    for res in allres],
+                   os.path.join(outdir, "gathered_gpu.pt"))
+    dist.barrier()
+    eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_two_rank_gpu_shard_equals_oracle(tmp_path):
+    """The multi-GPU path with the HIP engine (2 ranks on one GPU): gathered
+    decision records == the oracle's single-process results, every POC."""
+    port = free_port()
+    mp.spawn(gpu_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    got = torch.load(os.path.join(tmp_path, "gathered_gpu.pt"), weights_only=True)
+    orig, recon = synth.synth_sequence(W, H, NF, QP, seed=7)
+    assert len(got) == NF
+    for poc in range(1, NF + 1):
+        want = poc_results(orig, recon, poc)
+        g = got[poc - 1]
+        for (r, m), (c, p) in want.items():
+            gc, gp = g[f"{r}:{m}"]
+            assert torch.equal(gc, c) and torch.equal(gp, p), (poc, r, m)
