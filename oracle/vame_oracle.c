@@ -431,7 +431,11 @@ static void solve_equal(double a[7][7], int n, double *p) {
       break;
     }
     double temp = 0;
+#ifdef VAME_ORACLE_NO_FMA /* T5 probe build: the uncontracted alternative */
+    for (int j = i + 1; j < n; j++) temp = temp + a[i + 1][j] * p[j];
+#else
     for (int j = i + 1; j < n; j++) temp = fma(a[i + 1][j], p[j], temp); /* FP_CONTRACT */
+#endif
     p[i] = (a[i + 1][n] - temp) / a[i + 1][i];
   }
 }
