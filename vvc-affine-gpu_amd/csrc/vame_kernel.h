@@ -1246,7 +1246,10 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 
   // ---- stage the reference region (+margin) into LDS, clamp-to-edge padded:
   // 16-byte chunks, every load of a thread issued before its first LDS store
-  for (int dupS = 0; dupS < ((VAME_DUP & 8) ? 2 : 1); dupS++) {
+  // a region wholly outside the frame (the bottom CTU row at 1080p) has no
+  // in-frame CU: nothing is predicted, its tile is never read
+  const bool regionOut = tx0 + C::MARGIN >= W || ty0 + C::MARGIN >= H;
+  for (int dupS = 0; dupS < ((VAME_DUP & 8) ? 2 : 1) && !regionOut; dupS++) {
     constexpr int CPR = C::TILE / 8;  // chunks per tile row
     constexpr int NCH = C::TILE * CPR;
     constexpr int PER = (NCH + C::THREADS - 1) / C::THREADS;
