@@ -123,6 +123,12 @@ struct KParams {
 #ifndef VAME_ORDER
 #define VAME_ORDER 3
 #endif
+#ifndef VAME_STAGE1
+#define VAME_STAGE1 1
+#endif
+#ifndef VAME_PKCLIP
+#define VAME_PKCLIP 1
+#endif
 #ifndef VAME_WAVES
 #define VAME_WAVES 4
 #endif
@@ -158,6 +164,12 @@ __shared__ int s_ph_done;
   } }
 #define PH_INIT { if (tid == 0) { s_ph_blk[0] = ~0ull; s_ph_blk[1] = 0; s_ph_blk[2] = 0; s_ph_done = 0; } }
 #define PH_START { if (lane == 0) atomicMin(&s_ph_blk[0], ph_t0); }
+#elif defined(VAME_ISA_MARKS)  // analysis builds: phase ends as comments in the ISA
+#define PH_DECL
+#define PH_MARK(i) asm volatile("; PHASE_END " #i);
+#define PH_FLUSH
+#define PH_INIT
+#define PH_START
 #else
 #define PH_DECL
 #define PH_MARK(i)
@@ -366,6 +378,15 @@ __device__ __forceinline__ void hrow_raw(const unsigned (&D)[5], const uint4& KA
 __device__ __forceinline__ unsigned pack_shr2(int lo, int hi) {
   unsigned d = (unsigned)(lo >> 2);
   asm("v_ashrrev_i32_sdwa %0, 2, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "
+      "src1_sel:DWORD"
+      : "+v"(d)
+      : "v"(hi));
+  return d;
+}
+// (lo >> 10) | (hi >> 10) << 16, the same way (arithmetic shifts).
+__device__ __forceinline__ unsigned pack_sra10(int lo, int hi) {
+  unsigned d = (unsigned)(lo >> 10);
+  asm("v_ashrrev_i32_sdwa %0, 10, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD "
       "src1_sel:DWORD"
       : "+v"(d)
       : "v"(hi));
@@ -624,10 +645,25 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
                   pr);
     }
   } else {
+#if VAME_PKCLIP
+    // clipPel on packed pairs: acc >> 10 lies well inside int16 (the taps'
+    // absolute sums are below 2^7 per pass), so pack first, then clamp both
+    // halves at once (4 instructions per pair instead of 5)
+    const short2v lo = {0, 0}, hi = {1023, 1023};
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      P[r].x = as_u(__builtin_elementwise_min(
+          __builtin_elementwise_max(as_s2(pack_sra10(acc[r][0], acc[r][1])), lo), hi));
+      P[r].y = as_u(__builtin_elementwise_min(
+          __builtin_elementwise_max(as_s2(pack_sra10(acc[r][2], acc[r][3])), lo), hi));
+    }
+    return satd_4x4(O, P);
+#else
 #pragma unroll
     for (int r = 0; r < 4; r++)
 #pragma unroll
       for (int c = 0; c < 4; c++) pr[r][c] = clampi(acc[r][c] >> 10, 0, 1023);  // clipPel
+#endif
   }
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -1226,6 +1262,60 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   const int W = p.W, H = p.H;
   const int ctuX = (ctu % p.ctusPerRow) * kCtu, ctuY = (ctu / p.ctusPerRow) * kCtu;
 
+#if VAME_STAGE1
+  // ---- one latency round: the region origin is read with scalar loads, so
+  // the reference tile's loads are in flight together with the item's
+  // descriptor loads, and one barrier publishes both
+  const int tx0 = ctuX + (int)it->rx - C::MARGIN, ty0 = ctuY + (int)it->ry - C::MARGIN;  // tile origin
+  const bool regionOut = tx0 + C::MARGIN >= W || ty0 + C::MARGIN >= H;
+  constexpr int CPR = C::TILE / 8;  // chunks per tile row
+  constexpr int NCH = C::TILE * CPR;
+  constexpr int PER = (NCH + C::THREADS - 1) / C::THREADS;
+  uint4 tv[PER];
+  // stage the reference region (+margin) into LDS, clamp-to-edge padded, in
+  // 16-byte chunks; a region wholly outside the frame (the bottom CTU row at
+  // 1080p) has no in-frame CU: nothing is predicted, its tile is never read
+  if (!regionOut) {
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+      const int ch = tid + j * C::THREADS;
+      if (ch < NCH) {
+        const int ty = ch / CPR, cx = (ch % CPR) * 8;
+        const int fy = clampi(ty0 + ty, 0, H - 1), fx = tx0 + cx;
+        const uint16_t* row = ref + (size_t)fy * W;
+        if (fx >= 0 && fx + 7 < W) {
+          tv[j] = *reinterpret_cast<const uint4*>(row + fx);
+        } else {
+          unsigned a[8];
+#pragma unroll
+          for (int m = 0; m < 8; m++) a[m] = row[clampi(fx + m, 0, W - 1)];
+          tv[j] = make_uint4(a[0] | (a[1] << 16), a[2] | (a[3] << 16), a[4] | (a[5] << 16),
+                             a[6] | (a[7] << 16));
+        }
+      }
+    }
+  }
+  if (tid < kMaxCu) s_cu[tid] = it->cu[tid];
+  if (tid < kMaxWaves) s_wave[tid] = it->wave[tid];
+  if (tid < 48) s_coef[tid] = reinterpret_cast<const uint4*>(&kCoefTab)[tid];
+  if (tid < 80) s_eqmap[tid] = kEqMap.v[tid];
+  if (tid == 0) s_hdr[0] = it->nCu | (it->coop << 8) | (it->nWaves << 16) | (it->logL << 24);
+  for (int i = tid; i < kMaxCu * kNumMom; i += C::THREADS) (&s_val[0][0])[i] = 0;
+  PH_INIT
+  if (!regionOut) {
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+      const int ch = tid + j * C::THREADS;
+      if (ch < NCH) *reinterpret_cast<uint4*>(&s_tile[(ch / CPR) * C::TP + (ch % CPR) * 8]) = tv[j];
+    }
+  }
+  __syncthreads();
+  PH_START
+  const int hdr = __builtin_amdgcn_readfirstlane(s_hdr[0]);
+  const int nCu = hdr & 0xFF, nWaves = (hdr >> 16) & 0xFF;
+  const bool coop = ((hdr >> 8) & 0xFF) != 0;
+  PH_MARK(kPhStage)
+#else
   if (tid < kMaxCu) s_cu[tid] = it->cu[tid];
   if (tid < kMaxWaves) s_wave[tid] = it->wave[tid];
   if (tid < 48) s_coef[tid] = reinterpret_cast<const uint4*>(&kCoefTab)[tid];
@@ -1280,6 +1370,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   }
   __syncthreads();
   PH_MARK(kPhStage)
+#endif
   if (!coop && wv >= nWaves) {  // wave-uniform: an autonomous wave without CUs
     PH_FLUSH
     return;
