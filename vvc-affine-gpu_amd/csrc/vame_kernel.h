@@ -129,6 +129,9 @@ struct KParams {
 #ifndef VAME_PKCLIP
 #define VAME_PKCLIP 1
 #endif
+#ifndef VAME_PKMAD
+#define VAME_PKMAD 1
+#endif
 #ifndef VAME_WAVES
 #define VAME_WAVES 4
 #endif
@@ -691,6 +694,13 @@ __device__ __forceinline__ uint4 ext_row(const uint2& p, unsigned left, unsigned
 // sums S = (gx.gx, gx.gy, gy.gy, gx.e, gy.e).  Samples are handled as packed
 // int16 pairs: |g| <= 4092 and |e| <= 1023 fit, and v_dot2_i32_i16 sums stay
 // below 2^28 (exact).
+// 2 a + b on both int16 halves in one v_pk_mad_i16 (op_sel_hi:0 on the inline
+// constant: its low half, 2, multiplies the high halves too)
+__device__ __forceinline__ short2v twice_plus(short2v a, short2v b) {
+  unsigned r;
+  asm("v_pk_mad_i16 %0, %1, 2, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(as_u(a)), "v"(as_u(b)));
+  return as_s2(r);
+}
 __device__ __forceinline__ void grad_sb(int sx, int sy, const Geo& g, const uint4 (&X)[6],
                                         const uint2 (&Orig)[4], int S[5]) {
   short2v O[6][3], E[6][2];
@@ -708,12 +718,20 @@ __device__ __forceinline__ void grad_sb(int sx, int sy, const Geo& g, const uint
     short2v Hd[6], Vs[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) {
-      Hd[i] = O[i][k + 1] - O[i][k];                      // p(c+1) - p(c-1)
-      Vs[i] = O[i][k] + E[i][k] + E[i][k] + O[i][k + 1];  // p(c-1) + 2 p(c) + p(c+1)
+      Hd[i] = O[i][k + 1] - O[i][k];  // p(c+1) - p(c-1)
+#if VAME_PKMAD
+      Vs[i] = twice_plus(E[i][k], O[i][k] + O[i][k + 1]);  // p(c-1) + 2 p(c) + p(c+1)
+#else
+      Vs[i] = O[i][k] + E[i][k] + E[i][k] + O[i][k + 1];
+#endif
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
+#if VAME_PKMAD
+      gx[r][k] = twice_plus(Hd[r + 1], Hd[r] + Hd[r + 2]);
+#else
       gx[r][k] = Hd[r] + Hd[r + 1] + Hd[r + 1] + Hd[r + 2];
+#endif
       gy[r][k] = Vs[r + 2] - Vs[r];
     }
   }
