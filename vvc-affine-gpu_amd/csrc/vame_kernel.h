@@ -132,6 +132,9 @@ struct KParams {
 #ifndef VAME_PKMAD
 #define VAME_PKMAD 1
 #endif
+#ifndef VAME_RATE_UPD
+#define VAME_RATE_UPD 1
+#endif
 #ifndef VAME_WAVES
 #define VAME_WAVES 4
 #endif
@@ -948,7 +951,7 @@ struct CuState {
   int32_t satd;
   int32_t inframe;
   int32_t live;
-  int32_t pad;
+  int32_t rate;  // calc_affine_bits of cur (VAME_RATE_UPD: set at init and by the update)
 };
 
 template <int REGION>
@@ -1486,6 +1489,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       }
       st.bestCost = (long long)costInit;
       st.satd = 0;
+#if VAME_RATE_UPD
+      st.rate = affine_bits(c, ncp);
+#endif
       st.inframe = (cx + (1 << cs.lw) <= W) && (cy + (1 << cs.lh) <= H);
       st.live = st.inframe;
     }
@@ -1550,6 +1556,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         opaque(locR);
         const CuState& sr = s_st[cuR < 0 ? 0 : cuR];
         const bool rate = cuR >= 0 && (iter == 0 || sr.live);
+#if !VAME_RATE_UPD
         if (rate && locR < 2 * ncp) {
           int v = to_quarter(sr.cur[locR]);
           if (locR >= 2) v -= to_quarter(sr.cur[locR & 1]);
@@ -1558,9 +1565,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         b += dpp32<0x111, 0xF>(b);  // row_shr:1, 2, 4: lane 7 of the CU sums lanes 0..7
         b += dpp32<0x112, 0xF>(b);
         b += dpp32<0x114, 0xF>(b);
+#endif
         int better = 0;
         if (myCu >= 0 && local == 7) {
           CuState& st = s_st[myCu];
+#if VAME_RATE_UPD
+          b = st.rate;
+#endif
           if (rate) {
             const float prod = __fmul_rn(pa.lambda, (float)(b + kRuiBits));
             const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
@@ -1656,7 +1667,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         bool liveNew = false;
         if (act && loc < 8) {
           CuState& st = s_st[cuS];
-          int f = 0;
+          int f = 0, q = 0;
           if (loc < 2 * ncp) {  // 2 CP: LB stays (0, 0)
             const int j = loc;
             const double d = M[j == 1 ? 2 : j == 2 ? 1 : j];
@@ -1668,13 +1679,27 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             f = (v != cj ? 1 : 0) | (v != pj ? 16 : 0);
             st.prev[j] = cj;
             st.cur[j] = v;
+            q = to_quarter(v);
           }
+#if VAME_RATE_UPD
+          // the rate of the new CPMVs (calc_affine_bits, aux_functions.cl:2140-2189)
+          // rides on the same lane sum: component j codes q_j - q_(j & 1) for
+          // j >= 2 (RT - LT from lane j - 2, LB - LT from lane j - 4)
+          {
+            const int q2 = dpp32<0x112, 0xF>(q), q4 = dpp32<0x114, 0xF>(q);
+            if (loc < 2 * ncp) f += eg_bits(q - (loc >= 4 ? q4 : loc >= 2 ? q2 : 0)) << 8;
+          }
+#endif
           f += dpp32<0x111, 0xF>(f);  // row_shr:1, 2, 4: lane 7 sums lanes 0..7
           f += dpp32<0x112, 0xF>(f);
           f += dpp32<0x114, 0xF>(f);
           if (loc == 7) {
-            liveNew = (f & 15) != 0 && (f >> 4) != 0;  // moved, and not back to the previous
+            // moved, and not back to the previous (flag fields: bits 0-3 and 4-7)
+            liveNew = (f & 15) != 0 && ((f >> 4) & 15) != 0;
             st.live = liveNew;
+#if VAME_RATE_UPD
+            st.rate = f >> 8;
+#endif
           }
         }
         if (!coop) {  // leave once every CU of this wave is settled (wave-local)
