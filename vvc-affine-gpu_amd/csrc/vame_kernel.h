@@ -108,21 +108,24 @@ struct KParams {
 #endif
 // VAME_DUP (timing-only builds, results stay correct): run a phase twice to
 // price it in throughput terms: bit 0 prediction, bit 1 gradient, bit 2
-// equation reduction, bit 3 tile staging, bit 4 the solve (on a copy of the
-// system).
+// equation reduction, bit 3 tile staging (VAME_STAGE1=0 only), bit 4 the solve
+// (on a copy of the system).
 #ifndef VAME_DUP
 #define VAME_DUP 0
 #endif
-// quadrant kernel occupancy target (waves per SIMD; caps the VGPRs)
 // wave priority (s_setprio) during the latency-bound solve (0 = off): its
 // dependent FP64 / LDS chain issues ahead of other waves' prediction work
 // (~0.5 %; priority over the whole post-prediction part measured the same)
 #ifndef VAME_PRIO
 #define VAME_PRIO 3
 #endif
+// item-major block order (bit 0: 128-class kernel, bit 1: quadrant kernel)
 #ifndef VAME_ORDER
 #define VAME_ORDER 3
 #endif
+// A/B switches, default on; 0 builds the previous form for re-measurement
+// (DESIGN.md §5 progress table): one-latency-round prologue, packed clipPel,
+// Sobel [1 2 1] taps on v_pk_mad_i16, rate bits computed in the CPMV update
 #ifndef VAME_STAGE1
 #define VAME_STAGE1 1
 #endif
@@ -135,6 +138,7 @@ struct KParams {
 #ifndef VAME_RATE_UPD
 #define VAME_RATE_UPD 1
 #endif
+// quadrant kernel occupancy target (waves per SIMD; caps the VGPRs)
 #ifndef VAME_WAVES
 #define VAME_WAVES 4
 #endif
