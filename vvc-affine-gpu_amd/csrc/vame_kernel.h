@@ -138,6 +138,13 @@ struct KParams {
 #ifndef VAME_RATE_UPD
 #define VAME_RATE_UPD 1
 #endif
+// int64 transposing butterfly for the equation sums: 1 = cooperative items and
+// autonomous 32 / 64-lane segments, 2 = cooperative items only (measured best:
+// the autonomous waves' value copies around the swaps cost what the int64
+// adds save), 0 = int32 halves everywhere
+#ifndef VAME_RED64
+#define VAME_RED64 2
+#endif
 // quadrant kernel occupancy target (waves per SIMD; caps the VGPRs)
 #ifndef VAME_WAVES
 #define VAME_WAVES 4
@@ -917,9 +924,9 @@ __device__ __forceinline__ void seg_solve(long long* V, double* M, const uint8_t
       const int vi = m & 0x7F;
       const double sc = (m & 0x80) ? 8.0 : 1.0;
       double x;
-      if (coop)
+      if (coop || (VAME_RED64 == 1 && Ls >= 32))  // int64 slots
         x = (double)V[vi];
-      else
+      else  // int32 halves (segments of 16 lanes)
         x = fma((double)V32[NV + vi], 16777216.0, (double)(unsigned)V32[vi]);
       M[e] = x * sc;
     }
@@ -1221,9 +1228,130 @@ __device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int
     }
   }
 }
+// The same transposing butterfly on whole int64 values (VAME_RED64, segments of
+// 32 / 64 lanes): no lo / hi split, and a permlane step costs two swaps and
+// one 64-bit add per value pair instead of two swaps and two adds; DPP steps
+// move both dwords.  Sums of |x| < 2^44 over <= 256 lanes: exact.
+template <int B>
+__device__ __forceinline__ long long sel_bit64(long long if0, long long if1) {
+  const int lo = sel_bit<B>((int)(unsigned long long)if0, (int)(unsigned long long)if1);
+  const int hi = sel_bit<B>((int)((unsigned long long)if0 >> 32), (int)((unsigned long long)if1 >> 32));
+  return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+template <int B>
+__device__ __forceinline__ long long partner64(long long v) {  // value of lane ^ 2^B (B < 4)
+  const int lo = (int)(unsigned long long)v, hi = (int)((unsigned long long)v >> 32);
+  int rl, rh;
+  if constexpr (B == 3) {
+    rl = dpp32<0x128, 0xF>(lo); rh = dpp32<0x128, 0xF>(hi);
+  } else if constexpr (B == 1) {
+    rl = dpp32<0x4E, 0xF>(lo); rh = dpp32<0x4E, 0xF>(hi);
+  } else if constexpr (B == 0) {
+    rl = dpp32<0xB1, 0xF>(lo); rh = dpp32<0xB1, 0xF>(hi);
+  } else {  // B == 2: row_shl:4 into banks 0/2, row_shr:4 into banks 1/3
+    rl = __builtin_amdgcn_update_dpp(0, lo, 0x104, 0xF, 0x5, false);
+    rl = __builtin_amdgcn_update_dpp(rl, lo, 0x114, 0xF, 0xA, false);
+    rh = __builtin_amdgcn_update_dpp(0, hi, 0x104, 0xF, 0x5, false);
+    rh = __builtin_amdgcn_update_dpp(rh, hi, 0x114, 0xF, 0xA, false);
+  }
+  return (long long)(((unsigned long long)(unsigned)rh << 32) | (unsigned)rl);
+}
+template <int B, int M>
+__device__ __forceinline__ void halve64(long long* x) {
+  constexpr int H = (M + 1) / 2;
+#pragma unroll
+  for (int j = 0; j < H; j++) {
+    const long long a = x[j], b = j + H < M ? x[j + H] : 0;
+    if constexpr (B >= 4) {
+      const unsigned al = (unsigned)(unsigned long long)a, ah = (unsigned)((unsigned long long)a >> 32);
+      const unsigned bl = (unsigned)(unsigned long long)b, bh = (unsigned)((unsigned long long)b >> 32);
+      const auto rl = B == 5 ? __builtin_amdgcn_permlane32_swap(al, bl, false, false)
+                             : __builtin_amdgcn_permlane16_swap(al, bl, false, false);
+      const auto rh = B == 5 ? __builtin_amdgcn_permlane32_swap(ah, bh, false, false)
+                             : __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
+      x[j] = (long long)(((unsigned long long)rh[0] << 32) | rl[0]) +
+             (long long)(((unsigned long long)rh[1] << 32) | rl[1]);
+    } else {
+      x[j] = sel_bit64<B>(a, b) + partner64<B>(sel_bit64<B>(b, a));
+    }
+  }
+}
+template <int LOGS, int STEP, int M>
+__device__ __forceinline__ void butterfly64(long long* x) {
+  if constexpr (STEP < LOGS) {
+    constexpr int B = Schedule<LOGS, M>::bit(STEP);
+    if constexpr (M > 1) {
+      halve64<B, M>(x);
+      butterfly64<LOGS, STEP + 1, ceil_half(M)>(x);
+    } else {
+      // a plain step over bit B (row_shr:2^B): the sum is valid in the lanes
+      // whose bit B is set
+      static_assert(B <= 2, "plain steps only on DPP row bits");
+      const int lo = (int)(unsigned long long)x[0], hi = (int)((unsigned long long)x[0] >> 32);
+      const int rl = dpp32<0x110 + (1 << B), 0xF>(lo), rh = dpp32<0x110 + (1 << B), 0xF>(hi);
+      x[0] += (long long)(((unsigned long long)(unsigned)rh << 32) | (unsigned)rl);
+      butterfly64<LOGS, STEP + 1, M>(x);
+    }
+  }
+}
+template <int NCP, int LOGS, bool COOP>
+__device__ __forceinline__ void reduce_equations_64(const int (&S)[5], int u, int v, bool owner,
+                                                    long long* dst) {
+  constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
+  long long x[NV];
+#pragma unroll
+  for (int i = 0; i < NV; i++) x[i] = eq_value<NCP>(i, S, u, v);
+  butterfly64<LOGS, 0, NV>(x);
+  constexpr int CNT = Final<LOGS, NV>::count();
+  const int lidx = __lane_id() & ((1 << LOGS) - 1);
+  int off, limit;
+  held_window<LOGS, NV>(lidx, off, limit);
+  // the plain steps' bits (after the count reached 1) must be set
+  constexpr int kPlain = [] {
+    int m = NV, mask = 0;
+    for (int i = 0; i < LOGS; i++) {
+      if (m > 1)
+        m = ceil_half(m);
+      else
+        mask |= 1 << Schedule<LOGS, NV>::bit(i);
+    }
+    return mask;
+  }();
+  const bool ok = owner && (lidx & kPlain) == kPlain;
+  if (ok) {
+#pragma unroll
+    for (int j = 0; j < CNT; j++) {
+      const int idx = off + j;
+      if (idx < limit) {
+        if constexpr (COOP)
+          atomicAdd(reinterpret_cast<unsigned long long*>(&dst[idx]), (unsigned long long)x[j]);
+        else
+          dst[idx] = x[j];  // int64 slots
+      }
+    }
+  }
+}
+
 template <int NCP>
 __device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v, int logS,
                                                  bool owner, bool coop, long long* dst) {
+#if VAME_RED64
+  if (coop) {  // cooperative items: whole-wave segments, partial sums meet in LDS atomics
+    reduce_equations_64<NCP, 6, true>(S, u, v, owner, dst);
+    return;
+  }
+  switch (logS) {  // wave-uniform; autonomous waves hold CUs of 16, 32 or 64 sub-blocks
+    case 4: reduce_equations_c<NCP, 4, false>(S, u, v, owner, dst); break;
+    case 5:
+      if constexpr (VAME_RED64 == 1) reduce_equations_64<NCP, 5, false>(S, u, v, owner, dst);
+      else reduce_equations_c<NCP, 5, false>(S, u, v, owner, dst);
+      break;
+    default:
+      if constexpr (VAME_RED64 == 1) reduce_equations_64<NCP, 6, false>(S, u, v, owner, dst);
+      else reduce_equations_c<NCP, 6, false>(S, u, v, owner, dst);
+      break;
+  }
+#else
   if (coop) {  // cooperative items: whole-wave segments, partial sums meet in LDS atomics
     reduce_equations_c<NCP, 6, true>(S, u, v, owner, dst);
     return;
@@ -1233,6 +1361,7 @@ __device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v
     case 5: reduce_equations_c<NCP, 5, false>(S, u, v, owner, dst); break;
     default: reduce_equations_c<NCP, 6, false>(S, u, v, owner, dst); break;
   }
+#endif
 }
 
 
