@@ -142,6 +142,11 @@ struct KParams {
 // autonomous 32 / 64-lane segments, 2 = cooperative items only (measured best:
 // the autonomous waves' value copies around the swaps cost what the int64
 // adds save), 0 = int32 halves everywhere
+// opaque() recomputation per phase (bit 0 prediction geometry, 1 gradient
+// geometry, 2 cost indices, 3 reduction slot, 4 solve indices)
+#ifndef VAME_OPQ
+#define VAME_OPQ 17
+#endif
 #ifndef VAME_RED64
 #define VAME_RED64 2
 #endif
@@ -1642,7 +1647,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       if (live && !(VAME_ABLATE & 8)) {
         Geo gp = g;
         int sxp = sx, syp = sy;
-        opaque_geo(gp, sxp, syp);
+        if (VAME_OPQ & 1) opaque_geo(gp, sxp, syp);
         int cp[6];
         for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
         const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
@@ -1685,8 +1690,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       {
         int b = 0;
         int cuR = myCu, locR = local;  // recomputed addresses (no loop-carried copies)
-        opaque(cuR);
-        opaque(locR);
+        if (VAME_OPQ & 4) { opaque(cuR); opaque(locR); }
         const CuState& sr = s_st[cuR < 0 ? 0 : cuR];
         const bool rate = cuR >= 0 && (iter == 0 || sr.live);
 #if !VAME_RATE_UPD
@@ -1734,7 +1738,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           X[5] = ext_row(bt, dpp32<0x138, 0xF>((int)bt.y), dpp32<0x130, 0xF>((int)bt.x));
           Geo gg = g;
           int sxg = sx, syg = sy;
-          opaque_geo(gg, sxg, syg);
+          if (VAME_OPQ & 2) opaque_geo(gg, sxg, syg);
           grad_sb(sxg, syg, gg, X, Og, S);
           if (VAME_DUP & 2) {
             int S2[5];
@@ -1746,7 +1750,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         }
         if (!(VAME_ABLATE & 4)) {
           int cuV = myCu;
-          opaque(cuV);
+          if (VAME_OPQ & 8) opaque(cuV);
           long long* dst = s_val[cuV < 0 ? 0 : cuV];
           if (ncp == 2)
             reduce_equations<2>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
@@ -1770,8 +1774,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       if (!(VAME_ABLATE & 1)) {
         // the CU's lanes in its first wave solve it together
         int cuS = myCu, loc = local;
-        opaque(cuS);
-        opaque(loc);
+        if (VAME_OPQ & 16) { opaque(cuS); opaque(loc); }
         const bool solver = cuS >= 0 && loc < 64;
         const bool act = solver && s_st[cuS].live;
         const int Ls = 1 << logS;
