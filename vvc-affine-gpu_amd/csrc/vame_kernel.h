@@ -144,6 +144,9 @@ struct KParams {
 // adds save), 0 = int32 halves everywhere
 // opaque() recomputation per phase (bit 0 prediction geometry, 1 gradient
 // geometry, 2 cost indices, 3 reduction slot, 4 solve indices)
+#ifndef VAME_OPQ_ALL
+#define VAME_OPQ_ALL 1
+#endif
 #ifndef VAME_OPQ
 #define VAME_OPQ 17
 #endif
@@ -356,8 +359,13 @@ struct Geo {       // a lane's CU
 // iteration loop would pin ~60 VGPRs; recomputing them per phase is a few adds.
 __device__ __forceinline__ void opaque(int& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void opaque_geo(Geo& g, int& sx, int& sy) {
-  opaque(g.x); opaque(g.y); opaque(g.lw); opaque(g.lh);
-  opaque(g.w); opaque(g.h); opaque(sx); opaque(sy);
+  opaque(g.x); opaque(g.y); opaque(sx); opaque(sy);
+#if VAME_OPQ_ALL & 1
+  opaque(g.lw); opaque(g.lh);
+#endif
+#if VAME_OPQ_ALL & 2
+  opaque(g.w); opaque(g.h);
+#endif
 }
 
 
@@ -1197,6 +1205,7 @@ __device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int
   // j): fused with producing the value, so only NV halves are ever live
   constexpr int B0 = Schedule<LOGS, K>::bit(0);
   int x[K];
+#endif
 #pragma unroll
   for (int i = 0; i < NV; i++) {
     const long long e = eq_value<NCP>(i, S, u, v);
