@@ -1205,7 +1205,6 @@ __device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int
   // j): fused with producing the value, so only NV halves are ever live
   constexpr int B0 = Schedule<LOGS, K>::bit(0);
   int x[K];
-#endif
 #pragma unroll
   for (int i = 0; i < NV; i++) {
     const long long e = eq_value<NCP>(i, S, u, v);
