@@ -144,6 +144,9 @@ struct KParams {
 // adds save), 0 = int32 halves everywhere
 // opaque() recomputation per phase (bit 0 prediction geometry, 1 gradient
 // geometry, 2 cost indices, 3 reduction slot, 4 solve indices)
+#ifndef VAME_MASKDPP
+#define VAME_MASKDPP 1
+#endif
 #ifndef VAME_OPQ_ALL
 #define VAME_OPQ_ALL 1
 #endif
@@ -1057,8 +1060,8 @@ __device__ __forceinline__ int seg_sum_c(int v) {
 // partner lane (lane ^ 2^b), which keeps the second half -- so each step
 // halves the values a lane holds and doubles the lanes they are summed over.
 // Steps run in order of cost: bit 5 (v_permlane32_swap, 2 instructions per
-// exchanged pair), bit 4 (v_permlane16_swap), bit 3 (DPP row_ror:8), bits 1
-// and 0 (DPP quad_perm), bit 2 (two banked DPP moves).  After the last step
+// exchanged pair), bit 4 (v_permlane16_swap), bits 3 and 2 (two bank-masked
+// DPP adds), bits 1 and 0 (two selects and a DPP quad_perm add).  After the last step
 // every half is held, fully summed, by exactly one lane of the segment, which
 // stores it (autonomous items: int32 slots) or adds it (cooperative items:
 // int64 LDS atomics across waves).  Integer sums: the order is free.
@@ -1094,6 +1097,25 @@ __device__ __forceinline__ int xchg_dpp(int keep, int send) {
   return keep + r;
 }
 
+// Bits 3 / 2 of the lane are bank bits of the DPP row (banks 2-3 / 1-3), so
+// one exchange is two bank-masked DPP adds into the same register: the lanes
+// with the bit clear get a + partner(a), the others b + partner(b) (a lane's
+// DPP source reads happen before any lane writes).  Hazard waits are explicit:
+// the backend does not look inside inline asm.
+template <int B>
+__device__ __forceinline__ int xchg_masked(int a, int b) {
+  int r = a;
+  if constexpr (B == 3) {
+    asm("s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0x3" : "+v"(r));
+    asm("s_nop 1\n\tv_add_u32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0xc" : "+v"(r) : "v"(b));
+  } else {
+    static_assert(B == 2, "bank bits only");
+    asm("s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shl:4 row_mask:0xf bank_mask:0x5" : "+v"(r));
+    asm("s_nop 1\n\tv_add_u32_dpp %0, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xa" : "+v"(r) : "v"(b));
+  }
+  return r;
+}
+
 // Halving step over lane bit B on the first M values of x (the rest unused):
 // afterwards x[0 .. ceil(M/2)) holds this lane's kept half.
 template <int B, int M>
@@ -1112,7 +1134,10 @@ __device__ __forceinline__ void halve(int* x) {
 #pragma unroll
     for (int j = 0; j < H; j++) {
       const int a = x[j], b = j + H < M ? x[j + H] : 0;
-      x[j] = xchg_dpp<B>(sel_bit<B>(a, b), sel_bit<B>(b, a));
+      if constexpr (VAME_MASKDPP && (B == 3 || B == 2))
+        x[j] = xchg_masked<B>(a, b);
+      else
+        x[j] = xchg_dpp<B>(sel_bit<B>(a, b), sel_bit<B>(b, a));
     }
   }
 }
@@ -1122,10 +1147,16 @@ constexpr int ceil_half(int m) { return (m + 1) / 2; }
 // Step schedule per segment size: bits (in order) and the count after them.
 template <int LOGS, int K>
 struct Schedule {
-  // bit order: 5 4 3 1 0 2 restricted to bits < LOGS
+  // bit order restricted to bits < LOGS, cheapest exchanges first (while the
+  // counts are largest): 5 4 3 2 1 0 with the bank-masked DPP pairs of bits
+  // 3 / 2 (VAME_MASKDPP), else 5 4 3 1 0 2
   static constexpr int NB = LOGS;
   static constexpr int bit(int i) {
+#if VAME_MASKDPP
+    constexpr int all[6] = {5, 4, 3, 2, 1, 0};
+#else
     constexpr int all[6] = {5, 4, 3, 1, 0, 2};
+#endif
     int n = 0;
     for (int k = 0; k < 6; k++)
       if (all[k] < LOGS) {
@@ -1148,14 +1179,16 @@ __device__ __forceinline__ void butterfly(int* x) {
       halve<B, M>(x);
       butterfly<LOGS, STEP + 1, ceil_half(M)>(x);
     } else {
-      static_assert(B == 2, "plain steps only on bit 2");
-      x[0] += dpp32<0x114, 0xF>(x[0]);  // row_shr:4: banks 1/3 hold the sum
+      // a plain step over bit B (row_shr:2^B): the sum is valid in the lanes
+      // whose bit B is set
+      static_assert(B <= 2, "plain steps only on DPP row bits");
+      x[0] += dpp32<0x110 + (1 << B), 0xF>(x[0]);
       butterfly<LOGS, STEP + 1, M>(x);
     }
   }
 }
 
-// Count left per lane after the schedule, and whether a plain step ran.
+// Count left per lane after the schedule.
 template <int LOGS, int M, int STEP = 0>
 struct Final {
   static constexpr int count() {
@@ -1163,15 +1196,6 @@ struct Final {
     for (int i = 0; i < LOGS; i++)
       if (m > 1) m = ceil_half(m);
     return m;
-  }
-  static constexpr bool plain() {
-    int m = M, halvings = 0;
-    for (int i = 0; i < LOGS; i++)
-      if (m > 1) {
-        m = ceil_half(m);
-        halvings++;
-      }
-    return halvings < LOGS;
   }
 };
 
@@ -1213,6 +1237,8 @@ __device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int
       const auto r = B0 == 5 ? __builtin_amdgcn_permlane32_swap((unsigned)lo, (unsigned)hi, false, false)
                              : __builtin_amdgcn_permlane16_swap((unsigned)lo, (unsigned)hi, false, false);
       x[i] = (int)(r[0] + r[1]);
+    } else if constexpr (VAME_MASKDPP && (B0 == 3 || B0 == 2)) {
+      x[i] = xchg_masked<B0>(lo, hi);
     } else {
       x[i] = xchg_dpp<B0>(sel_bit<B0>(lo, hi), sel_bit<B0>(hi, lo));
     }
@@ -1222,8 +1248,18 @@ __device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int
   const int lidx = __lane_id() & ((1 << LOGS) - 1);
   int off, limit;
   held_window<LOGS, K>(lidx, off, limit);
-  bool ok = owner;
-  if constexpr (Final<LOGS, K>::plain()) ok = ok && ((lidx >> 2) & 1);
+  // the plain steps' bits (after the count reached 1) must be set
+  constexpr int kPlain = [] {
+    int m = K, mask = 0;
+    for (int i = 0; i < LOGS; i++) {
+      if (m > 1)
+        m = ceil_half(m);
+      else
+        mask |= 1 << Schedule<LOGS, K>::bit(i);
+    }
+    return mask;
+  }();
+  const bool ok = owner && (lidx & kPlain) == kPlain;
   if (ok) {
 #pragma unroll
     for (int j = 0; j < CNT; j++) {
