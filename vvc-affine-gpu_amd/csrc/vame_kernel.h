@@ -242,10 +242,13 @@ __device__ __forceinline__ void clip_mv(int& x, int& y, int bx, int by, int W, i
 }
 
 // aux_functions.cl:106-141 (bipred == 0)
-__device__ __forceinline__ bool spread_over_limit(int a, int b, int c, int d) {
+__device__ __forceinline__ bool spread_over_limit(int a, int b, int c, int d, bool six) {
   const int s4 = 4 << 11;
   int w = (abs(4 * a + s4) >> 11) + 9, h = (abs(4 * b) >> 11) + 9;
   if (w * h > 165) return true;
+  // 2 CP: (c, d) = (-b, a), so the second test's w and h are the first's h and
+  // w -- the same product
+  if (!six) return false;
   w = (abs(4 * c) >> 11) + 9;
   h = (abs(4 * d + s4) >> 11) + 9;
   return w * h > 165;
@@ -346,7 +349,7 @@ __device__ __forceinline__ MvField mv_field(const int* cp, int ncp, int lw, int 
     f.vx = -f.hy;
     f.vy = f.hx;
   }
-  f.spread = spread_over_limit(f.hx, f.hy, f.vx, f.vy);
+  f.spread = spread_over_limit(f.hx, f.hy, f.vx, f.vy, ncp == 3);
   f.bx = shl(cp[0], 7);
   f.by = shl(cp[1], 7);
   return f;
