@@ -93,7 +93,8 @@ def test_kernel_ab_switches_compile(tmp_path):
     import subprocess
     src = os.path.join(os.path.dirname(__file__), "..", "vvc-affine-gpu_amd", "csrc", "vame_engine.hip")
     defs = ["-DVAME_STAGE1=0", "-DVAME_PKCLIP=0", "-DVAME_PKMAD=0", "-DVAME_RATE_UPD=0",
-            "-DVAME_RED64=0", "-DVAME_OPQ=31", "-DVAME_OPQ_ALL=3"]
+            "-DVAME_RED64=0", "-DVAME_OPQ=31", "-DVAME_OPQ_ALL=3",
+            "-DVAME_MASKDPP=0", "-DVAME_PASS_T=0"]
     r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O1", "-std=c++17",
                         "-ffp-contract=off", "--cuda-device-only", "-c", *defs, "-o",
                         str(tmp_path / "ab.o"), src], capture_output=True, text=True, timeout=600)

@@ -144,6 +144,9 @@ struct KParams {
 // adds save), 0 = int32 halves everywhere
 // opaque() recomputation per phase (bit 0 prediction geometry, 1 gradient
 // geometry, 2 cost indices, 3 reduction slot, 4 solve indices)
+#ifndef VAME_PASS_T
+#define VAME_PASS_T 1
+#endif
 #ifndef VAME_MASKDPP
 #define VAME_MASKDPP 1
 #endif
@@ -1625,9 +1628,16 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   const int sbTop = max(sbIdx - sbCols, 0), sbBot = min(sbIdx + sbCols, C::NSB - 1);
   const bool leader = myCu >= 0 && (lane & ((1 << logS) - 1)) == (1 << logS) - 1;
 
+#if VAME_PASS_T
+  // one copy of the pass per CP count: ncp is a compile-time constant in each,
+  // so the 2-CP pass carries none of the 3-CP selects and branches
+  auto run_pass = [&](auto ncpTag) {
+    constexpr int ncp = decltype(ncpTag)::value;
+#else
   for (int pass = 0; pass < 2; pass++) {
     const int ncp = pass == 0 ? 2 : 3;
     if ((pass == 0 && !p.run2) || (pass == 1 && !p.run3)) continue;
+#endif
     const int niter = (ncp == 3 ? 4 : 5) + p.extra;
 
     // ---- per-CU initial CPMVs (2 CP: zero; 3 CP: derived from the 2-CP winner)
@@ -1919,7 +1929,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     }
     phase_sync(coop);
     PH_MARK(kPhTail)
+#if VAME_PASS_T
+  };
+  if (p.run2) run_pass(std::integral_constant<int, 2>{});
+  if (p.run3) run_pass(std::integral_constant<int, 3>{});
+#else
   }
+#endif
   PH_FLUSH
 }
 
