@@ -144,8 +144,10 @@ struct KParams {
 // adds save), 0 = int32 halves everywhere
 // opaque() recomputation per phase (bit 0 prediction geometry, 1 gradient
 // geometry, 2 cost indices, 3 reduction slot, 4 solve indices)
+// pass body instantiations: 1 = per CP count, 2 = per CP count and item class
+// (autonomous / cooperative), 0 = one runtime-generic body
 #ifndef VAME_PASS_T
-#define VAME_PASS_T 1
+#define VAME_PASS_T 2
 #endif
 #ifndef VAME_MASKDPP
 #define VAME_MASKDPP 1
@@ -1631,8 +1633,11 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 #if VAME_PASS_T
   // one copy of the pass per CP count: ncp is a compile-time constant in each,
   // so the 2-CP pass carries none of the 3-CP selects and branches
-  auto run_pass = [&](auto ncpTag) {
+  auto run_pass = [&](auto ncpTag, auto coopTag) {
     constexpr int ncp = decltype(ncpTag)::value;
+#if VAME_PASS_T >= 2
+    constexpr bool coop = decltype(coopTag)::value;  // and per item class
+#endif
 #else
   for (int pass = 0; pass < 2; pass++) {
     const int ncp = pass == 0 ? 2 : 3;
@@ -1931,8 +1936,18 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     PH_MARK(kPhTail)
 #if VAME_PASS_T
   };
-  if (p.run2) run_pass(std::integral_constant<int, 2>{});
-  if (p.run3) run_pass(std::integral_constant<int, 3>{});
+#if VAME_PASS_T >= 2
+  if (coop) {
+    if (p.run2) run_pass(std::integral_constant<int, 2>{}, std::true_type{});
+    if (p.run3) run_pass(std::integral_constant<int, 3>{}, std::true_type{});
+  } else {
+    if (p.run2) run_pass(std::integral_constant<int, 2>{}, std::false_type{});
+    if (p.run3) run_pass(std::integral_constant<int, 3>{}, std::false_type{});
+  }
+#else
+  if (p.run2) run_pass(std::integral_constant<int, 2>{}, std::false_type{});
+  if (p.run3) run_pass(std::integral_constant<int, 3>{}, std::false_type{});
+#endif
 #else
   }
 #endif
