@@ -252,7 +252,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
   // two streams so they overlap; VAME_BIG_STREAM picks which one the 128-class
   // kernel is issued on (0: side stream, after an event; 1: caller's stream,
   // first, with the quadrant kernel on the side stream).  A 128-class
-  // workgroup needs a whole CU (16 waves, 92 KB LDS): issued first, its
+  // workgroup needs a whole CU (16 waves, 81 KB LDS): issued first, its
   // workgroups take CUs before the quadrant ones fill them, and the small
   // quadrant workgroups, not the long 128-class ones, make the tail
   // (batched c2 step 1.32 -> 1.245 ms).

@@ -1961,7 +1961,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VAME_W
     KParams p) {
   affine_me_body<64, false>(p);
 }
-// 128-class items: one 1024-thread workgroup per CU (94 KB of LDS), one lane
+// 128-class items: one 1024-thread workgroup per CU (81 KB of LDS), one lane
 // per sub-block of a 128x128 CU.
 __global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_body<128, false>(p); }
 // The same with PROF (vame_set_prof).
