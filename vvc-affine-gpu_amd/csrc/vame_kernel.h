@@ -149,8 +149,9 @@ struct KParams {
 #ifndef VAME_PASS_T
 #define VAME_PASS_T 2
 #endif
+// bank-masked DPP exchanges: 1 = int32 reductions, 2 = also the int64 ones
 #ifndef VAME_MASKDPP
-#define VAME_MASKDPP 1
+#define VAME_MASKDPP 2
 #endif
 #ifndef VAME_OPQ_ALL
 #define VAME_OPQ_ALL 1
@@ -1313,6 +1314,33 @@ __device__ __forceinline__ long long partner64(long long v) {  // value of lane 
   }
   return (long long)(((unsigned long long)(unsigned)rh << 32) | (unsigned)rl);
 }
+// The bank-masked exchange (xchg_masked) on int64 values: each 64-bit add is
+// v_add_co / v_addc_co with DPP; the carry in VCC stays within the lanes one
+// masked pair enables.
+template <int B>
+__device__ __forceinline__ long long xchg_masked64(long long a, long long b) {
+  unsigned al = (unsigned)(unsigned long long)a, ah = (unsigned)((unsigned long long)a >> 32);
+  const unsigned bl = (unsigned)(unsigned long long)b, bh = (unsigned)((unsigned long long)b >> 32);
+  if constexpr (B == 3) {
+    asm("s_nop 1\n\tv_add_co_u32_dpp %0, vcc, %0, %0 row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
+        "s_nop 1\n\tv_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
+        "s_nop 1\n\tv_add_co_u32_dpp %0, vcc, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
+        "s_nop 1\n\tv_addc_co_u32_dpp %1, vcc, %3, %3, vcc row_ror:8 row_mask:0xf bank_mask:0xc"
+        : "+v"(al), "+v"(ah)
+        : "v"(bl), "v"(bh)
+        : "vcc");
+  } else {
+    static_assert(B == 2, "bank bits only");
+    asm("s_nop 1\n\tv_add_co_u32_dpp %0, vcc, %0, %0 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+        "s_nop 1\n\tv_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+        "s_nop 1\n\tv_add_co_u32_dpp %0, vcc, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+        "s_nop 1\n\tv_addc_co_u32_dpp %1, vcc, %3, %3, vcc row_shr:4 row_mask:0xf bank_mask:0xa"
+        : "+v"(al), "+v"(ah)
+        : "v"(bl), "v"(bh)
+        : "vcc");
+  }
+  return (long long)(((unsigned long long)ah << 32) | al);
+}
 template <int B, int M>
 __device__ __forceinline__ void halve64(long long* x) {
   constexpr int H = (M + 1) / 2;
@@ -1328,6 +1356,8 @@ __device__ __forceinline__ void halve64(long long* x) {
                              : __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
       x[j] = (long long)(((unsigned long long)rh[0] << 32) | rl[0]) +
              (long long)(((unsigned long long)rh[1] << 32) | rl[1]);
+    } else if constexpr (VAME_MASKDPP >= 2 && (B == 3 || B == 2)) {
+      x[j] = xchg_masked64<B>(a, b);
     } else {
       x[j] = sel_bit64<B>(a, b) + partner64<B>(sel_bit64<B>(b, a));
     }
