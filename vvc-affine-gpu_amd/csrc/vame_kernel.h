@@ -159,8 +159,11 @@ struct KParams {
 #ifndef VAME_OPQ
 #define VAME_OPQ 17
 #endif
+// int64 transposing butterfly for the equation sums: 1 = cooperative items and
+// autonomous 32 / 64-lane segments (best once bits 3 / 2 use the bank-masked
+// DPP pairs), 2 = cooperative items only, 0 = int32 halves everywhere
 #ifndef VAME_RED64
-#define VAME_RED64 2
+#define VAME_RED64 1
 #endif
 // quadrant kernel occupancy target (waves per SIMD; caps the VGPRs)
 #ifndef VAME_WAVES
