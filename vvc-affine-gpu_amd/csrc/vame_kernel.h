@@ -161,9 +161,10 @@ struct KParams {
 #endif
 // int64 transposing butterfly for the equation sums: 1 = cooperative items and
 // autonomous 32 / 64-lane segments (best once bits 3 / 2 use the bank-masked
-// DPP pairs), 2 = cooperative items only, 0 = int32 halves everywhere
+// DPP pairs), 3 = every segment, 2 = cooperative items only, 0 = int32 halves
+// everywhere
 #ifndef VAME_RED64
-#define VAME_RED64 1
+#define VAME_RED64 3
 #endif
 // quadrant kernel occupancy target (waves per SIMD; caps the VGPRs)
 #ifndef VAME_WAVES
@@ -952,7 +953,7 @@ __device__ __forceinline__ void seg_solve(long long* V, double* M, const uint8_t
       const int vi = m & 0x7F;
       const double sc = (m & 0x80) ? 8.0 : 1.0;
       double x;
-      if (coop || (VAME_RED64 == 1 && Ls >= 32))  // int64 slots
+      if (coop || (VAME_RED64 == 1 && Ls >= 32) || VAME_RED64 == 3)  // int64 slots
         x = (double)V[vi];
       else  // int32 halves (segments of 16 lanes)
         x = fma((double)V32[NV + vi], 16777216.0, (double)(unsigned)V32[vi]);
@@ -1431,13 +1432,16 @@ __device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v
     return;
   }
   switch (logS) {  // wave-uniform; autonomous waves hold CUs of 16, 32 or 64 sub-blocks
-    case 4: reduce_equations_c<NCP, 4, false>(S, u, v, owner, dst); break;
+    case 4:
+      if constexpr (VAME_RED64 == 3) reduce_equations_64<NCP, 4, false>(S, u, v, owner, dst);
+      else reduce_equations_c<NCP, 4, false>(S, u, v, owner, dst);
+      break;
     case 5:
-      if constexpr (VAME_RED64 == 1) reduce_equations_64<NCP, 5, false>(S, u, v, owner, dst);
+      if constexpr (VAME_RED64 == 1 || VAME_RED64 == 3) reduce_equations_64<NCP, 5, false>(S, u, v, owner, dst);
       else reduce_equations_c<NCP, 5, false>(S, u, v, owner, dst);
       break;
     default:
-      if constexpr (VAME_RED64 == 1) reduce_equations_64<NCP, 6, false>(S, u, v, owner, dst);
+      if constexpr (VAME_RED64 == 1 || VAME_RED64 == 3) reduce_equations_64<NCP, 6, false>(S, u, v, owner, dst);
       else reduce_equations_c<NCP, 6, false>(S, u, v, owner, dst);
       break;
   }
