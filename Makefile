@@ -17,9 +17,15 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
 LIB_SRCS := $(CSRC)/vame_engine.hip $(CSRC)/vame_hostlogic.cpp $(CSRC)/vame_io.cpp
 LIB_HDRS := $(CSRC)/vame_kernel.h $(CSRC)/vame_tables.h include/vame.h
 
-all: lib cli oracle
+all: lib cli synth oracle
 
 lib: $(LIBDIR)/libvame.so
+
+# synthetic test-sequence generator (bench / tests only; vame/synth.py is its spec)
+synth: $(LIBDIR)/libvame_synth.so
+$(LIBDIR)/libvame_synth.so: $(CSRC)/vame_synth.c
+	@mkdir -p $(LIBDIR)
+	gcc -O2 -fopenmp -ffp-contract=off -fPIC -shared -Wall -o $@ $<
 
 # timing-only ablation builds (results are wrong): make ablate [ABLATE_SET="..."]
 ABLATE_SET ?= 1 2 4 6 7 8 11 13 14 15 16 32
@@ -57,4 +63,4 @@ clean:
 	rm -rf $(LIBDIR) $(BINDIR)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all lib cli oracle clean resource-usage ablate phase variant
+.PHONY: all lib cli synth oracle clean resource-usage ablate phase variant

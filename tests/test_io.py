@@ -85,6 +85,16 @@ def test_read_frames_errors_and_raw(tmp_path):
     short.write_text("1,2\n" * 240)
     with pytest.raises(Exception):
         logs.read_frames(str(short), 3, 240, 1)
+    # stoi's out_of_range: a value beyond int's range is rejected, not wrapped
+    for big in ("2147483648", "-2147483649", "99999999999999999999999"):
+        over = tmp_path / "over.csv"
+        over.write_text(f"1,{big},3\n" * 240)
+        with pytest.raises(Exception):
+            logs.read_frames(str(over), 3, 240, 1)
+    edge = tmp_path / "edge.csv"  # int's own limits are accepted (stored as unsigned short)
+    edge.write_text("2147483647,-2147483648,65537\n" * 240)
+    got = logs.read_frames(str(edge), 3, 240, 1)
+    assert (got[0, :, 0] == 0xFFFF).all() and (got[0, :, 1] == 0).all() and (got[0, :, 2] == 1).all()
     raw = str(tmp_path / "f.u16")
     fr.tofile(raw)
     assert (logs.read_frames(raw, 416, 240, 1) == fr).all()

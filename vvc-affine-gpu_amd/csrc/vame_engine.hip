@@ -14,19 +14,6 @@
 #include "../../include/vame.h"
 #include "vame_kernel.h"
 
-#ifndef VAME_PAD8
-#define VAME_PAD8 1
-#endif
-#ifndef VAME_TFLAGS
-#define VAME_TFLAGS hipEventDisableSystemFence
-#endif
-#ifndef VAME_JFLAGS
-#define VAME_JFLAGS 0
-#endif
-#ifndef VAME_BIG_STREAM
-#define VAME_BIG_STREAM 1
-#endif
-
 using namespace vame;
 
 static_assert(sizeof(vame_cpmvs) == 28, "Cpmvs layout (typedef.h)");
@@ -222,8 +209,8 @@ int time_begin(vame_ctx* c, int cls, hipStream_t s) {
     std::pair<hipEvent_t, hipEvent_t> e;
     // timing-only events: no system-scope fence (no cache writeback /
     // invalidation between the kernels they bracket)
-    VAME_HIP(hipEventCreateWithFlags(&e.first, VAME_TFLAGS));
-    VAME_HIP(hipEventCreateWithFlags(&e.second, VAME_TFLAGS));
+    VAME_HIP(hipEventCreateWithFlags(&e.first, hipEventDisableSystemFence));
+    VAME_HIP(hipEventCreateWithFlags(&e.second, hipEventDisableSystemFence));
     v.push_back(e);
   }
   VAME_HIP(hipEventRecord(v[c->evUsed[cls]].first, s));
@@ -236,6 +223,23 @@ int time_end(vame_ctx* c, int cls, hipStream_t s) {
   return VAME_OK;
 }
 
+// Makes c->device current for one C-ABI call and restores the caller's device
+// on every return path: the entry points must not change the calling thread's
+// current device (a torch thread holding engines on two GPUs would otherwise
+// see torch.cuda.current_device() move under it).
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err;
+  explicit DeviceGuard(int dev) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int now = -1;
+    if (prev >= 0 && hipGetDevice(&now) == hipSuccess && now != prev) (void)hipSetDevice(prev);
+  }
+};
+
 #define VAME_TRY(x)        \
   do {                     \
     int rc_ = (x);         \
@@ -243,15 +247,15 @@ int time_end(vame_ctx* c, int cls, hipStream_t s) {
   } while (0)
 
 // (ctu, pair) blocks per template item, padded to a multiple of 8 (one per
-// XCD) under VAME_PAD8 so every item of a CTU lands on the same XCD
-int combos(int n) { return VAME_PAD8 ? (n + 7) / 8 * 8 : n; }
+// XCD) so every item of a CTU lands on the same XCD (the kernel's item-major
+// block order; padding blocks exit at once)
+int combos(int n) { return (n + 7) / 8 * 8; }
 
 int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
            hipStream_t stream) {
   // 128-class items (big LDS, 1 workgroup per CU) and quadrant items run on
-  // two streams so they overlap; VAME_BIG_STREAM picks which one the 128-class
-  // kernel is issued on (0: side stream, after an event; 1: caller's stream,
-  // first, with the quadrant kernel on the side stream).  A 128-class
+  // two streams so they overlap: the 128-class kernel on the caller's stream,
+  // first, and the quadrant kernel on the side stream.  A 128-class
   // workgroup needs a whole CU (16 waves, 81 KB LDS): issued first, its
   // workgroups take CUs before the quadrant ones fill them, and the small
   // quadrant workgroups, not the long 128-class ones, make the tail
@@ -263,7 +267,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
   if (fork) {
     VAME_HIP(hipEventRecord(c->evFork, stream));
     VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
-    if (VAME_BIG_STREAM) sQuad = c->side; else sBig = c->side;
+    sQuad = c->side;
   }
   auto big = [&]() -> int {
     KParams kb = kp;
@@ -347,7 +351,8 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   int ndev = 0;
   VAME_HIP(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return VAME_E_INVALID;
-  VAME_HIP(hipSetDevice(device));
+  DeviceGuard guard(device);
+  VAME_HIP(guard.err);
   std::vector<Item> big, qf, qh;
   build_templates(big, qf, qh);
   vame_ctx* c = new vame_ctx();
@@ -366,8 +371,8 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (e == hipSuccess) e = hipMemcpy(c->dQuad, quad.data(), quad.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->dBig, big.data(), big.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming | VAME_JFLAGS);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming | VAME_JFLAGS);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming);
   if (e != hipSuccess) {
     snprintf(g_hip_err, sizeof(g_hip_err), "%s", hipGetErrorString(e));
     vame_destroy(c);
@@ -379,7 +384,7 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
 
 void vame_destroy(vame_ctx* c) {
   if (!c) return;
-  (void)hipSetDevice(c->device);
+  DeviceGuard guard(c->device);
   if (c->dQuad) (void)hipFree(c->dQuad);
   if (c->dBig) (void)hipFree(c->dBig);
   if (c->side) (void)hipStreamDestroy(c->side);
@@ -400,7 +405,8 @@ int vame_affine_me(vame_ctx* c, const uint16_t* ref, const uint16_t* cur, float 
   if ((align != 0 && align != 1) || (nCP != 2 && nCP != 3) || extra < 0 || extra > 64)
     return VAME_E_INVALID;
   if (nCP == 3 && !prev) return VAME_E_INVALID;
-  VAME_HIP(hipSetDevice(c->device));
+  DeviceGuard guard(c->device);
+  VAME_HIP(guard.err);
   KParams kp;
   memset(&kp, 0, sizeof(kp));
   fill_common(kp, c, extra);
@@ -435,7 +441,8 @@ int vame_affine_me_batch(vame_ctx* c, const vame_poc_job* jobs, int njobs, int m
       }
     }
   }
-  VAME_HIP(hipSetDevice(c->device));
+  DeviceGuard guard(c->device);
+  VAME_HIP(guard.err);
   // every (POC, refIdx) pair of the batch, kMaxPairs per launch
   KParams kp;
   memset(&kp, 0, sizeof(kp));
@@ -486,7 +493,8 @@ int vame_set_timing(vame_ctx* c, int enable) {
 
 int vame_get_timing(vame_ctx* c, int cls, double* total_ms, int* launches, int reset) {
   if (!c || cls < 0 || cls > 1 || !total_ms || !launches) return VAME_E_INVALID;
-  VAME_HIP(hipSetDevice(c->device));
+  DeviceGuard guard(c->device);
+  VAME_HIP(guard.err);
   double t = 0;
   for (size_t i = 0; i < c->evUsed[cls]; i++) {
     float ms = 0;

@@ -96,8 +96,14 @@ bool parse_line(const char* s, const char* e, int W, uint16_t* out) {
     bool neg = false;
     if (s < e && (*s == '-' || *s == '+')) neg = *s++ == '-';
     if (s >= e || *s < '0' || *s > '9') return false;
-    long v = 0;
-    while (s < e && *s >= '0' && *s <= '9') v = v * 10 + (*s++ - '0');
+    // std::stoi semantics (main.cpp:324): a value outside int's range throws
+    // out_of_range there, so it is rejected here (bounded: no overflow)
+    const long long lim = neg ? 2147483648ll : 2147483647ll;
+    long long v = 0;
+    while (s < e && *s >= '0' && *s <= '9') {
+      v = v * 10 + (*s++ - '0');
+      if (v > lim) return false;
+    }
     out[w] = (uint16_t)(neg ? -v : v);  // stored into unsigned short (main.cpp:324-325)
     while (s < e && *s != ',') s++;
     if (s < e) s++;  // the ','

@@ -98,6 +98,7 @@ struct KParams {
   int run2, run3;
 };
 
+// Instrumentation builds only (the product build sets neither):
 // VAME_ABLATE (timing-only builds, results are wrong): bit 0 skip the solve,
 // bit 1 skip the gradient math, bit 2 skip the reductions of the equations,
 // bit 3 skip the prediction math, bit 4 skip the 128-class launch, bit 5 skip
@@ -108,72 +109,15 @@ struct KParams {
 #endif
 // VAME_DUP (timing-only builds, results stay correct): run a phase twice to
 // price it in throughput terms: bit 0 prediction, bit 1 gradient, bit 2
-// equation reduction, bit 3 tile staging (VAME_STAGE1=0 only), bit 4 the solve
-// (on a copy of the system).
+// equation reduction, bit 4 the solve (on a copy of the system).
 #ifndef VAME_DUP
 #define VAME_DUP 0
 #endif
-// wave priority (s_setprio) during the latency-bound solve (0 = off): its
-// dependent FP64 / LDS chain issues ahead of other waves' prediction work
-// (~0.5 %; priority over the whole post-prediction part measured the same)
-#ifndef VAME_PRIO
-#define VAME_PRIO 3
-#endif
-// item-major block order (bit 0: 128-class kernel, bit 1: quadrant kernel)
-#ifndef VAME_ORDER
-#define VAME_ORDER 3
-#endif
-// A/B switches, default on; 0 builds the previous form for re-measurement
-// (DESIGN.md §5 progress table): one-latency-round prologue, packed clipPel,
-// Sobel [1 2 1] taps on v_pk_mad_i16, rate bits computed in the CPMV update
-#ifndef VAME_STAGE1
-#define VAME_STAGE1 1
-#endif
-#ifndef VAME_PKCLIP
-#define VAME_PKCLIP 1
-#endif
-#ifndef VAME_PKMAD
-#define VAME_PKMAD 1
-#endif
-#ifndef VAME_RATE_UPD
-#define VAME_RATE_UPD 1
-#endif
-// int64 transposing butterfly for the equation sums: 1 = cooperative items and
-// autonomous 32 / 64-lane segments, 2 = cooperative items only (measured best:
-// the autonomous waves' value copies around the swaps cost what the int64
-// adds save), 0 = int32 halves everywhere
-// opaque() recomputation per phase (bit 0 prediction geometry, 1 gradient
-// geometry, 2 cost indices, 3 reduction slot, 4 solve indices)
-// pass body instantiations: 1 = per CP count, 2 = per CP count and item class
-// (autonomous / cooperative), 0 = one runtime-generic body
-#ifndef VAME_PASS_T
-#define VAME_PASS_T 2
-#endif
-// bank-masked DPP exchanges: 1 = int32 reductions, 2 = also the int64 ones
-#ifndef VAME_MASKDPP
-#define VAME_MASKDPP 2
-#endif
-#ifndef VAME_OPQ_ALL
-#define VAME_OPQ_ALL 1
-#endif
-#ifndef VAME_OPQ
-#define VAME_OPQ 17
-#endif
-// int64 transposing butterfly for the equation sums: 1 = cooperative items and
-// autonomous 32 / 64-lane segments (best once bits 3 / 2 use the bank-masked
-// DPP pairs), 3 = every segment, 2 = cooperative items only, 0 = int32 halves
-// everywhere
-#ifndef VAME_RED64
-#define VAME_RED64 3
-#endif
-// quadrant kernel occupancy target (waves per SIMD; caps the VGPRs)
-#ifndef VAME_WAVES
-#define VAME_WAVES 4
-#endif
-// LDS reference-tile margin of the quadrant kernel (samples)
-#ifndef VAME_QMARGIN
-#define VAME_QMARGIN 16
-#endif
+// Wave priority (s_setprio) during the latency-bound solve: its dependent
+// FP64 / LDS chain issues ahead of other waves' prediction work (~0.5 %;
+// priority 1 / 3 and priority over the whole post-prediction part measured
+// the same).
+constexpr int kSolvePrio = 3;
 
 // VAME_PHASE_TIMING (profiling-only builds, libvame_phase.so): every wave sums
 // the shader clock spent per phase and adds it to g_phase_cycles at exit.
@@ -376,12 +320,7 @@ struct Geo {       // a lane's CU
 __device__ __forceinline__ void opaque(int& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void opaque_geo(Geo& g, int& sx, int& sy) {
   opaque(g.x); opaque(g.y); opaque(sx); opaque(sy);
-#if VAME_OPQ_ALL & 1
   opaque(g.lw); opaque(g.lh);
-#endif
-#if VAME_OPQ_ALL & 2
-  opaque(g.w); opaque(g.h);
-#endif
 }
 
 
@@ -691,7 +630,6 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
                   pr);
     }
   } else {
-#if VAME_PKCLIP
     // clipPel on packed pairs: acc >> 10 lies well inside int16 (the taps'
     // absolute sums are below 2^7 per pass), so pack first, then clamp both
     // halves at once (4 instructions per pair instead of 5)
@@ -704,12 +642,6 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
           __builtin_elementwise_max(as_s2(pack_sra10(acc[r][2], acc[r][3])), lo), hi));
     }
     return satd_4x4(O, P);
-#else
-#pragma unroll
-    for (int r = 0; r < 4; r++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) pr[r][c] = clampi(acc[r][c] >> 10, 0, 1023);  // clipPel
-#endif
   }
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -761,20 +693,12 @@ __device__ __forceinline__ void grad_sb(int sx, int sy, const Geo& g, const uint
     short2v Hd[6], Vs[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) {
-      Hd[i] = O[i][k + 1] - O[i][k];  // p(c+1) - p(c-1)
-#if VAME_PKMAD
+      Hd[i] = O[i][k + 1] - O[i][k];                       // p(c+1) - p(c-1)
       Vs[i] = twice_plus(E[i][k], O[i][k] + O[i][k + 1]);  // p(c-1) + 2 p(c) + p(c+1)
-#else
-      Vs[i] = O[i][k] + E[i][k] + E[i][k] + O[i][k + 1];
-#endif
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-#if VAME_PKMAD
       gx[r][k] = twice_plus(Hd[r + 1], Hd[r] + Hd[r + 2]);
-#else
-      gx[r][k] = Hd[r] + Hd[r + 1] + Hd[r + 1] + Hd[r + 2];
-#endif
       gy[r][k] = Vs[r + 2] - Vs[r];
     }
   }
@@ -937,27 +861,18 @@ constexpr EqMap make_eq_map() {
 __constant__ EqMap kEqMap = make_eq_map();
 
 // Build, eliminate and back-substitute one CU's system with its segment; the
-// segment's first lane returns the deltas.  The integer sums convert exactly
-// (|value| < 2^53): autonomous items hold them as int32 halves, value =
-// hi * 2^24 + lo, formed in double as fma(hi, 2^24, lo) (both terms exact, the
-// sum exact); the right-hand side is scaled by 8 exactly.
+// segment's first lane returns the deltas.  The int64 sums convert exactly
+// (|value| < 2^53); the right-hand side is scaled by 8 exactly.
 template <int NCP, bool KEEP_V = false>
 __device__ __forceinline__ void seg_solve(long long* V, double* M, const uint8_t* eqmap, int li,
                                           int Ls, bool act, bool coop, int lw, int lh,
                                           double dd[6]) {
-  constexpr int N = 2 * NCP, NC = N + 1, NV = NCP == 2 ? kNumVal2 : kNumMom;
+  constexpr int N = 2 * NCP, NC = N + 1;
   if (act) {
-    const int* V32 = reinterpret_cast<const int*>(V);
     for (int e = li; e < N * NC; e += Ls) {
       const int m = eqmap[(NCP == 2 ? 0 : 32) + e];
-      const int vi = m & 0x7F;
       const double sc = (m & 0x80) ? 8.0 : 1.0;
-      double x;
-      if (coop || (VAME_RED64 == 1 && Ls >= 32) || VAME_RED64 == 3)  // int64 slots
-        x = (double)V[vi];
-      else  // int32 halves (segments of 16 lanes)
-        x = fma((double)V32[NV + vi], 16777216.0, (double)(unsigned)V32[vi]);
-      M[e] = x * sc;
+      M[e] = (double)V[m & 0x7F] * sc;
     }
     if (!KEEP_V && coop && li < kNumMom) {  // cooperative items accumulate with atomics
       int z = 0;
@@ -991,13 +906,13 @@ struct CuState {
   int32_t satd;
   int32_t inframe;
   int32_t live;
-  int32_t rate;  // calc_affine_bits of cur (VAME_RATE_UPD: set at init and by the update)
+  int32_t rate;  // calc_affine_bits of cur (set at init and by the update)
 };
 
 template <int REGION>
 struct Cfg {
   static constexpr int THREADS = REGION == 128 ? 1024 : 256;  // workgroup size = sub-blocks
-  static constexpr int MARGIN = REGION == 128 ? 16 : VAME_QMARGIN;  // reference-tile margin
+  static constexpr int MARGIN = 16;                     // reference-tile margin (samples)
   static constexpr int TILE = REGION + 2 * MARGIN;      // tile edge (samples)
   // tile pitch (samples) == 8 (mod 16): the window rows of sub-blocks 4 rows
   // apart land 16 banks apart (2-way at most for the packed-pair reads)
@@ -1064,263 +979,54 @@ __device__ __forceinline__ int seg_sum_c(int v) {
 }
 
 // Reduction of a CU's equations over its sub-blocks (one per lane), as a
-// transposing butterfly.  Each int64 value x is split into two int32 halves,
-// x = hi * 2^24 + lo with lo in [0, 2^24): |x| < 2^44, so over at most 64
-// lanes sum(lo) < 2^30 and |sum(hi)| < 2^26 -- exact.  The K = 2 * NV halves
-// of every lane are then summed over the segment (the CU's lanes in this
-// wave) by halving exchanges: at a step over lane bit b, the lanes with bit b
-// clear keep the first half of their values and send the second half to the
-// partner lane (lane ^ 2^b), which keeps the second half -- so each step
-// halves the values a lane holds and doubles the lanes they are summed over.
-// Steps run in order of cost: bit 5 (v_permlane32_swap, 2 instructions per
-// exchanged pair), bit 4 (v_permlane16_swap), bits 3 and 2 (two bank-masked
-// DPP adds), bits 1 and 0 (two selects and a DPP quad_perm add).  After the last step
-// every half is held, fully summed, by exactly one lane of the segment, which
-// stores it (autonomous items: int32 slots) or adds it (cooperative items:
-// int64 LDS atomics across waves).  Integer sums: the order is free.
-template <int M>
-struct HalfVals {
-  int v[M];
-};
+// transposing butterfly on whole int64 values (sums of |x| < 2^44 over <= 256
+// lanes: exact).  The NV values of every lane are summed over the segment
+// (the CU's lanes in this wave) by halving exchanges: at a step over lane bit
+// b, the lanes with bit b clear keep the first half of their values and send
+// the second half to the partner lane (lane ^ 2^b), which keeps the second
+// half -- so each step halves the values a lane holds and doubles the lanes
+// they are summed over.  Steps run cheapest first, while the counts are
+// largest: bit 5 (v_permlane32_swap), bit 4 (v_permlane16_swap), bits 3 and 2
+// (two bank-masked DPP add pairs), bits 1 and 0 (selects and a DPP quad_perm
+// add).  After the last step every value is held, fully summed, by exactly one
+// lane of the segment, which stores it (autonomous items: int64 slots) or adds
+// it (cooperative items: int64 LDS atomics across waves).  Integer sums: the
+// order is free.
 
 // Lane-bit selects: lane l gets (l >> B) & 1 ? if1 : if0.  Issued as the VOP3
 // v_cndmask_b32 with the constant lane mask in an SGPR pair: the VOP2 form the
 // compiler picks (condition in VCC) runs ~3x slower when two follow each other
 // (profiles/ubench/valu_rate.hip: 7.7 vs 2.5 SIMD cycles per instruction in
 // the reductions' select-select-DPP pattern).
-constexpr unsigned long long kLaneBitMask[6] = {0xAAAAAAAAAAAAAAAAull, 0xCCCCCCCCCCCCCCCCull,
-                                                0xF0F0F0F0F0F0F0F0ull, 0xFF00FF00FF00FF00ull,
-                                                0xFFFF0000FFFF0000ull, 0xFFFFFFFF00000000ull};
+constexpr unsigned long long kLaneBitMask[2] = {0xAAAAAAAAAAAAAAAAull, 0xCCCCCCCCCCCCCCCCull};
 template <int B>
 __device__ __forceinline__ int sel_bit(int if0, int if1) {
   int r;
   asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(kLaneBitMask[B]));
   return r;
 }
-
-// One exchange over lane bit B via DPP: returns keep + partner(send).
-template <int B>
-__device__ __forceinline__ int xchg_dpp(int keep, int send) {
-  if constexpr (B == 3) return keep + dpp32<0x128, 0xF>(send);  // row_ror:8 == lane ^ 8
-  if constexpr (B == 1) return keep + dpp32<0x4E, 0xF>(send);   // quad_perm [2,3,0,1]
-  if constexpr (B == 0) return keep + dpp32<0xB1, 0xF>(send);   // quad_perm [1,0,3,2]
-  // B == 2: lane ^ 4 = row_shl:4 into banks 0/2, row_shr:4 into banks 1/3
-  int r = __builtin_amdgcn_update_dpp(0, send, 0x104, 0xF, 0x5, false);
-  r = __builtin_amdgcn_update_dpp(r, send, 0x114, 0xF, 0xA, false);
-  return keep + r;
-}
-
-// Bits 3 / 2 of the lane are bank bits of the DPP row (banks 2-3 / 1-3), so
-// one exchange is two bank-masked DPP adds into the same register: the lanes
-// with the bit clear get a + partner(a), the others b + partner(b) (a lane's
-// DPP source reads happen before any lane writes).  Hazard waits are explicit:
-// the backend does not look inside inline asm.
-template <int B>
-__device__ __forceinline__ int xchg_masked(int a, int b) {
-  int r = a;
-  if constexpr (B == 3) {
-    asm("s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0x3" : "+v"(r));
-    asm("s_nop 1\n\tv_add_u32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0xc" : "+v"(r) : "v"(b));
-  } else {
-    static_assert(B == 2, "bank bits only");
-    asm("s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shl:4 row_mask:0xf bank_mask:0x5" : "+v"(r));
-    asm("s_nop 1\n\tv_add_u32_dpp %0, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xa" : "+v"(r) : "v"(b));
-  }
-  return r;
-}
-
-// Halving step over lane bit B on the first M values of x (the rest unused):
-// afterwards x[0 .. ceil(M/2)) holds this lane's kept half.
-template <int B, int M>
-__device__ __forceinline__ void halve(int* x) {
-  constexpr int H = (M + 1) / 2;
-  if constexpr (B >= 4) {
-#pragma unroll
-    for (int j = 0; j < H; j++) {
-      const unsigned a = (unsigned)x[j], b = j + H < M ? (unsigned)x[j + H] : 0u;
-      // bit 5: lanes 0-31 end with a summed over (l, l^32), lanes 32-63 with b
-      const auto r = B == 5 ? __builtin_amdgcn_permlane32_swap(a, b, false, false)
-                            : __builtin_amdgcn_permlane16_swap(a, b, false, false);
-      x[j] = (int)(r[0] + r[1]);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < H; j++) {
-      const int a = x[j], b = j + H < M ? x[j + H] : 0;
-      if constexpr (VAME_MASKDPP && (B == 3 || B == 2))
-        x[j] = xchg_masked<B>(a, b);
-      else
-        x[j] = xchg_dpp<B>(sel_bit<B>(a, b), sel_bit<B>(b, a));
-    }
-  }
-}
-
-constexpr int ceil_half(int m) { return (m + 1) / 2; }
-
-// Step schedule per segment size: bits (in order) and the count after them.
-template <int LOGS, int K>
-struct Schedule {
-  // bit order restricted to bits < LOGS, cheapest exchanges first (while the
-  // counts are largest): 5 4 3 2 1 0 with the bank-masked DPP pairs of bits
-  // 3 / 2 (VAME_MASKDPP), else 5 4 3 1 0 2
-  static constexpr int NB = LOGS;
-  static constexpr int bit(int i) {
-#if VAME_MASKDPP
-    constexpr int all[6] = {5, 4, 3, 2, 1, 0};
-#else
-    constexpr int all[6] = {5, 4, 3, 1, 0, 2};
-#endif
-    int n = 0;
-    for (int k = 0; k < 6; k++)
-      if (all[k] < LOGS) {
-        if (n == i) return all[k];
-        n++;
-      }
-    return -1;
-  }
-};
-
-// Runs the halving steps while the count is > 1; returns (through x) the
-// values and reports how many halving steps ran.  A remaining segment bit
-// after the count reached 1 becomes a plain sum (valid in the lanes whose bit
-// is set).
-template <int LOGS, int STEP, int M>
-__device__ __forceinline__ void butterfly(int* x) {
-  if constexpr (STEP < LOGS) {
-    constexpr int B = Schedule<LOGS, M>::bit(STEP);
-    if constexpr (M > 1) {
-      halve<B, M>(x);
-      butterfly<LOGS, STEP + 1, ceil_half(M)>(x);
-    } else {
-      // a plain step over bit B (row_shr:2^B): the sum is valid in the lanes
-      // whose bit B is set
-      static_assert(B <= 2, "plain steps only on DPP row bits");
-      x[0] += dpp32<0x110 + (1 << B), 0xF>(x[0]);
-      butterfly<LOGS, STEP + 1, M>(x);
-    }
-  }
-}
-
-// Count left per lane after the schedule.
-template <int LOGS, int M, int STEP = 0>
-struct Final {
-  static constexpr int count() {
-    int m = M;
-    for (int i = 0; i < LOGS; i++)
-      if (m > 1) m = ceil_half(m);
-    return m;
-  }
-};
-
-// Window of value indices a lane holds after the schedule: [off, off + count),
-// valid below `limit` (the upper half of an odd count carries a zero pad).
-template <int LOGS, int K>
-__device__ __forceinline__ void held_window(int lidx, int& off, int& limit) {
-  off = 0;
-  limit = K;
-  int m = K;
-#pragma unroll
-  for (int i = 0; i < LOGS; i++) {
-    if (m <= 1) break;
-    const int b = Schedule<LOGS, K>::bit(i);
-    const int h = ceil_half(m);
-    if ((lidx >> b) & 1) {
-      off += h;
-    } else {
-      limit = off + h;
-    }
-    m = h;
-  }
-}
-
-template <int NCP, int LOGS, bool COOP>
-__device__ __forceinline__ void reduce_equations_c(const int (&S)[5], int u, int v, bool owner,
-                                                   long long* dst) {
-  constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
-  constexpr int K = 2 * NV;
-  // the first halving step pairs x[j] = lo(value j) with x[j + NV] = hi(value
-  // j): fused with producing the value, so only NV halves are ever live
-  constexpr int B0 = Schedule<LOGS, K>::bit(0);
-  int x[K];
-#pragma unroll
-  for (int i = 0; i < NV; i++) {
-    const long long e = eq_value<NCP>(i, S, u, v);
-    const int lo = (int)((unsigned)e & 0xFFFFFFu), hi = (int)(e >> 24);
-    if constexpr (B0 >= 4) {
-      const auto r = B0 == 5 ? __builtin_amdgcn_permlane32_swap((unsigned)lo, (unsigned)hi, false, false)
-                             : __builtin_amdgcn_permlane16_swap((unsigned)lo, (unsigned)hi, false, false);
-      x[i] = (int)(r[0] + r[1]);
-    } else if constexpr (VAME_MASKDPP && (B0 == 3 || B0 == 2)) {
-      x[i] = xchg_masked<B0>(lo, hi);
-    } else {
-      x[i] = xchg_dpp<B0>(sel_bit<B0>(lo, hi), sel_bit<B0>(hi, lo));
-    }
-  }
-  butterfly<LOGS, 1, NV>(x);
-  constexpr int CNT = Final<LOGS, K>::count();
-  const int lidx = __lane_id() & ((1 << LOGS) - 1);
-  int off, limit;
-  held_window<LOGS, K>(lidx, off, limit);
-  // the plain steps' bits (after the count reached 1) must be set
-  constexpr int kPlain = [] {
-    int m = K, mask = 0;
-    for (int i = 0; i < LOGS; i++) {
-      if (m > 1)
-        m = ceil_half(m);
-      else
-        mask |= 1 << Schedule<LOGS, K>::bit(i);
-    }
-    return mask;
-  }();
-  const bool ok = owner && (lidx & kPlain) == kPlain;
-  if (ok) {
-#pragma unroll
-    for (int j = 0; j < CNT; j++) {
-      const int idx = off + j;
-      if (idx < limit) {
-        if constexpr (COOP) {
-          const unsigned long long add =
-              idx < NV ? (unsigned long long)(unsigned)x[j]
-                       : (unsigned long long)((long long)x[j] * (1ll << 24));
-          atomicAdd(reinterpret_cast<unsigned long long*>(&dst[idx < NV ? idx : idx - NV]), add);
-        } else {
-          reinterpret_cast<int*>(dst)[idx] = x[j];  // int32 slots: lo[0..NV), hi[NV..2NV)
-        }
-      }
-    }
-  }
-}
-// The same transposing butterfly on whole int64 values (VAME_RED64, segments of
-// 32 / 64 lanes): no lo / hi split, and a permlane step costs two swaps and
-// one 64-bit add per value pair instead of two swaps and two adds; DPP steps
-// move both dwords.  Sums of |x| < 2^44 over <= 256 lanes: exact.
 template <int B>
 __device__ __forceinline__ long long sel_bit64(long long if0, long long if1) {
   const int lo = sel_bit<B>((int)(unsigned long long)if0, (int)(unsigned long long)if1);
   const int hi = sel_bit<B>((int)((unsigned long long)if0 >> 32), (int)((unsigned long long)if1 >> 32));
   return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
+// value of lane ^ 2^B for the quad bits (B < 2): DPP quad_perm
 template <int B>
-__device__ __forceinline__ long long partner64(long long v) {  // value of lane ^ 2^B (B < 4)
+__device__ __forceinline__ long long partner64(long long v) {
+  static_assert(B == 0 || B == 1, "quad bits only");
+  constexpr int ctrl = B == 1 ? 0x4E : 0xB1;  // quad_perm [2,3,0,1] / [1,0,3,2]
   const int lo = (int)(unsigned long long)v, hi = (int)((unsigned long long)v >> 32);
-  int rl, rh;
-  if constexpr (B == 3) {
-    rl = dpp32<0x128, 0xF>(lo); rh = dpp32<0x128, 0xF>(hi);
-  } else if constexpr (B == 1) {
-    rl = dpp32<0x4E, 0xF>(lo); rh = dpp32<0x4E, 0xF>(hi);
-  } else if constexpr (B == 0) {
-    rl = dpp32<0xB1, 0xF>(lo); rh = dpp32<0xB1, 0xF>(hi);
-  } else {  // B == 2: row_shl:4 into banks 0/2, row_shr:4 into banks 1/3
-    rl = __builtin_amdgcn_update_dpp(0, lo, 0x104, 0xF, 0x5, false);
-    rl = __builtin_amdgcn_update_dpp(rl, lo, 0x114, 0xF, 0xA, false);
-    rh = __builtin_amdgcn_update_dpp(0, hi, 0x104, 0xF, 0x5, false);
-    rh = __builtin_amdgcn_update_dpp(rh, hi, 0x114, 0xF, 0xA, false);
-  }
+  const int rl = dpp32<ctrl, 0xF>(lo), rh = dpp32<ctrl, 0xF>(hi);
   return (long long)(((unsigned long long)(unsigned)rh << 32) | (unsigned)rl);
 }
-// The bank-masked exchange (xchg_masked) on int64 values: each 64-bit add is
+// Bits 3 / 2 of the lane are bank bits of the DPP row (banks 2-3 / 1-3), so
+// one exchange is two bank-masked DPP adds into the same register: the lanes
+// with the bit clear get a + partner(a), the others b + partner(b) (a lane's
+// DPP source reads happen before any lane writes).  Each 64-bit add is
 // v_add_co / v_addc_co with DPP; the carry in VCC stays within the lanes one
-// masked pair enables.
+// masked pair enables.  Hazard waits are explicit: the backend does not look
+// inside inline asm.
 template <int B>
 __device__ __forceinline__ long long xchg_masked64(long long a, long long b) {
   unsigned al = (unsigned)(unsigned long long)a, ah = (unsigned)((unsigned long long)a >> 32);
@@ -1345,6 +1051,27 @@ __device__ __forceinline__ long long xchg_masked64(long long a, long long b) {
   }
   return (long long)(((unsigned long long)ah << 32) | al);
 }
+
+constexpr int ceil_half(int m) { return (m + 1) / 2; }
+
+// Step order for a segment of 2^LOGS lanes: bits 5 4 3 2 1 0, restricted to
+// bits < LOGS.
+template <int LOGS>
+struct Schedule {
+  static constexpr int bit(int i) {
+    constexpr int all[6] = {5, 4, 3, 2, 1, 0};
+    int n = 0;
+    for (int k = 0; k < 6; k++)
+      if (all[k] < LOGS) {
+        if (n == i) return all[k];
+        n++;
+      }
+    return -1;
+  }
+};
+
+// Halving step over lane bit B on the first M values of x (the rest unused):
+// afterwards x[0 .. ceil(M/2)) holds this lane's kept half.
 template <int B, int M>
 __device__ __forceinline__ void halve64(long long* x) {
   constexpr int H = (M + 1) / 2;
@@ -1354,29 +1081,31 @@ __device__ __forceinline__ void halve64(long long* x) {
     if constexpr (B >= 4) {
       const unsigned al = (unsigned)(unsigned long long)a, ah = (unsigned)((unsigned long long)a >> 32);
       const unsigned bl = (unsigned)(unsigned long long)b, bh = (unsigned)((unsigned long long)b >> 32);
+      // bit 5: lanes 0-31 end with a summed over (l, l^32), lanes 32-63 with b
       const auto rl = B == 5 ? __builtin_amdgcn_permlane32_swap(al, bl, false, false)
                              : __builtin_amdgcn_permlane16_swap(al, bl, false, false);
       const auto rh = B == 5 ? __builtin_amdgcn_permlane32_swap(ah, bh, false, false)
                              : __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
       x[j] = (long long)(((unsigned long long)rh[0] << 32) | rl[0]) +
              (long long)(((unsigned long long)rh[1] << 32) | rl[1]);
-    } else if constexpr (VAME_MASKDPP >= 2 && (B == 3 || B == 2)) {
+    } else if constexpr (B == 3 || B == 2) {
       x[j] = xchg_masked64<B>(a, b);
     } else {
       x[j] = sel_bit64<B>(a, b) + partner64<B>(sel_bit64<B>(b, a));
     }
   }
 }
+// Runs the halving steps while the count is > 1.  A remaining segment bit
+// after the count reached 1 becomes a plain sum (row_shr:2^B), valid in the
+// lanes whose bit is set.
 template <int LOGS, int STEP, int M>
 __device__ __forceinline__ void butterfly64(long long* x) {
   if constexpr (STEP < LOGS) {
-    constexpr int B = Schedule<LOGS, M>::bit(STEP);
+    constexpr int B = Schedule<LOGS>::bit(STEP);
     if constexpr (M > 1) {
       halve64<B, M>(x);
       butterfly64<LOGS, STEP + 1, ceil_half(M)>(x);
     } else {
-      // a plain step over bit B (row_shr:2^B): the sum is valid in the lanes
-      // whose bit B is set
       static_assert(B <= 2, "plain steps only on DPP row bits");
       const int lo = (int)(unsigned long long)x[0], hi = (int)((unsigned long long)x[0] >> 32);
       const int rl = dpp32<0x110 + (1 << B), 0xF>(lo), rh = dpp32<0x110 + (1 << B), 0xF>(hi);
@@ -1385,6 +1114,37 @@ __device__ __forceinline__ void butterfly64(long long* x) {
     }
   }
 }
+
+// Count left per lane after the schedule.
+template <int LOGS, int M>
+constexpr int final_count() {
+  int m = M;
+  for (int i = 0; i < LOGS; i++)
+    if (m > 1) m = ceil_half(m);
+  return m;
+}
+
+// Window of value indices a lane holds after the schedule: [off, off + count),
+// valid below `limit` (the upper half of an odd count carries a zero pad).
+template <int LOGS, int K>
+__device__ __forceinline__ void held_window(int lidx, int& off, int& limit) {
+  off = 0;
+  limit = K;
+  int m = K;
+#pragma unroll
+  for (int i = 0; i < LOGS; i++) {
+    if (m <= 1) break;
+    const int b = Schedule<LOGS>::bit(i);
+    const int h = ceil_half(m);
+    if ((lidx >> b) & 1) {
+      off += h;
+    } else {
+      limit = off + h;
+    }
+    m = h;
+  }
+}
+
 template <int NCP, int LOGS, bool COOP>
 __device__ __forceinline__ void reduce_equations_64(const int (&S)[5], int u, int v, bool owner,
                                                     long long* dst) {
@@ -1393,7 +1153,7 @@ __device__ __forceinline__ void reduce_equations_64(const int (&S)[5], int u, in
 #pragma unroll
   for (int i = 0; i < NV; i++) x[i] = eq_value<NCP>(i, S, u, v);
   butterfly64<LOGS, 0, NV>(x);
-  constexpr int CNT = Final<LOGS, NV>::count();
+  constexpr int CNT = final_count<LOGS, NV>();
   const int lidx = __lane_id() & ((1 << LOGS) - 1);
   int off, limit;
   held_window<LOGS, NV>(lidx, off, limit);
@@ -1404,7 +1164,7 @@ __device__ __forceinline__ void reduce_equations_64(const int (&S)[5], int u, in
       if (m > 1)
         m = ceil_half(m);
       else
-        mask |= 1 << Schedule<LOGS, NV>::bit(i);
+        mask |= 1 << Schedule<LOGS>::bit(i);
     }
     return mask;
   }();
@@ -1426,36 +1186,15 @@ __device__ __forceinline__ void reduce_equations_64(const int (&S)[5], int u, in
 template <int NCP>
 __device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v, int logS,
                                                  bool owner, bool coop, long long* dst) {
-#if VAME_RED64
   if (coop) {  // cooperative items: whole-wave segments, partial sums meet in LDS atomics
     reduce_equations_64<NCP, 6, true>(S, u, v, owner, dst);
     return;
   }
   switch (logS) {  // wave-uniform; autonomous waves hold CUs of 16, 32 or 64 sub-blocks
-    case 4:
-      if constexpr (VAME_RED64 == 3) reduce_equations_64<NCP, 4, false>(S, u, v, owner, dst);
-      else reduce_equations_c<NCP, 4, false>(S, u, v, owner, dst);
-      break;
-    case 5:
-      if constexpr (VAME_RED64 == 1 || VAME_RED64 == 3) reduce_equations_64<NCP, 5, false>(S, u, v, owner, dst);
-      else reduce_equations_c<NCP, 5, false>(S, u, v, owner, dst);
-      break;
-    default:
-      if constexpr (VAME_RED64 == 1 || VAME_RED64 == 3) reduce_equations_64<NCP, 6, false>(S, u, v, owner, dst);
-      else reduce_equations_c<NCP, 6, false>(S, u, v, owner, dst);
-      break;
+    case 4: reduce_equations_64<NCP, 4, false>(S, u, v, owner, dst); break;
+    case 5: reduce_equations_64<NCP, 5, false>(S, u, v, owner, dst); break;
+    default: reduce_equations_64<NCP, 6, false>(S, u, v, owner, dst); break;
   }
-#else
-  if (coop) {  // cooperative items: whole-wave segments, partial sums meet in LDS atomics
-    reduce_equations_c<NCP, 6, true>(S, u, v, owner, dst);
-    return;
-  }
-  switch (logS) {  // wave-uniform; autonomous waves hold CUs of 16, 32 or 64 sub-blocks
-    case 4: reduce_equations_c<NCP, 4, false>(S, u, v, owner, dst); break;
-    case 5: reduce_equations_c<NCP, 5, false>(S, u, v, owner, dst); break;
-    default: reduce_equations_c<NCP, 6, false>(S, u, v, owner, dst); break;
-  }
-#endif
 }
 
 
@@ -1483,24 +1222,17 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 
   // ---- XCD-aware block -> (ref, ctu, item): blocks b, b+8, ... share an XCD;
   // give each XCD a contiguous run of logical work (same CTUs -> L2 reuse).
-  const int nb = gridDim.x, b = blockIdx.x;
-  const int q8 = nb >> 3, r8 = nb & 7, xcd = b & 7;
-  int logical = xcd * q8 + min(xcd, r8) + (b >> 3);
-  int itemIdx = logical % p.nItems;
-  int rest = logical / p.nItems;
-  // Item-major dispatch order (VAME_ORDER bit 0: 128-class kernel, bit 1:
-  // quadrant kernel): all (ctu, pair) blocks of template item 0 first, then
-  // item 1, ...; the host lists the costlier items first, so the tail is made of
-  // short workgroups (blocks b, b+8, ... still spread over the XCDs).
-  if ((VAME_ORDER & (REGION == 128 ? 1 : 2)) != 0) {
-    // the host pads the (ctu, pair) combinations of an item to a multiple of
-    // 8 (VAME_PAD8), so combination j runs on XCD j % 8 for every item: the
-    // items of one CTU re-read its reference tile from the same L2
-    const int per = nb / p.nItems;
-    itemIdx = b / per;
-    rest = b % per;
-    if (rest >= p.nCtus * p.nPairs) return;  // padding block (uniform, before any barrier)
-  }
+  // Item-major dispatch order: all (ctu, pair) blocks of template item 0
+  // first, then item 1, ...; the host lists the costlier items first, so the
+  // tail is made of short workgroups.  The host pads the (ctu, pair)
+  // combinations of an item to a multiple of 8, so combination j runs on XCD
+  // j % 8 (blocks are dealt round-robin over the 8 XCDs) for every item: the
+  // items of one CTU re-read its reference tile from the same L2.
+  const int b = blockIdx.x;
+  const int per = (int)gridDim.x / p.nItems;
+  const int itemIdx = b / per;
+  const int rest = b % per;
+  if (rest >= p.nCtus * p.nPairs) return;  // padding block (uniform, before any barrier)
   const int ctu = rest % p.nCtus;
   const int pairIdx = rest / p.nCtus;  // (POC, refIdx) pair of this launch
   const PairArgs& pa = p.pair[pairIdx];
@@ -1510,7 +1242,6 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   const int W = p.W, H = p.H;
   const int ctuX = (ctu % p.ctusPerRow) * kCtu, ctuY = (ctu / p.ctusPerRow) * kCtu;
 
-#if VAME_STAGE1
   // ---- one latency round: the region origin is read with scalar loads, so
   // the reference tile's loads are in flight together with the item's
   // descriptor loads, and one barrier publishes both
@@ -1563,62 +1294,6 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   const int nCu = hdr & 0xFF, nWaves = (hdr >> 16) & 0xFF;
   const bool coop = ((hdr >> 8) & 0xFF) != 0;
   PH_MARK(kPhStage)
-#else
-  if (tid < kMaxCu) s_cu[tid] = it->cu[tid];
-  if (tid < kMaxWaves) s_wave[tid] = it->wave[tid];
-  if (tid < 48) s_coef[tid] = reinterpret_cast<const uint4*>(&kCoefTab)[tid];
-  if (tid < 80) s_eqmap[tid] = kEqMap.v[tid];
-  if (tid == 0) {
-    s_hdr[0] = it->nCu | (it->coop << 8) | (it->nWaves << 16) | (it->logL << 24);
-    s_hdr[2] = it->rx;
-    s_hdr[3] = it->ry;
-  }
-  for (int i = tid; i < kMaxCu * kNumMom; i += C::THREADS) (&s_val[0][0])[i] = 0;
-  PH_INIT
-  __syncthreads();
-  PH_START
-  const int hdr = __builtin_amdgcn_readfirstlane(s_hdr[0]);
-  const int nCu = hdr & 0xFF, nWaves = (hdr >> 16) & 0xFF;
-  const bool coop = ((hdr >> 8) & 0xFF) != 0;
-  const int tx0 = ctuX + s_hdr[2] - C::MARGIN, ty0 = ctuY + s_hdr[3] - C::MARGIN;  // tile origin
-
-  // ---- stage the reference region (+margin) into LDS, clamp-to-edge padded:
-  // 16-byte chunks, every load of a thread issued before its first LDS store
-  // a region wholly outside the frame (the bottom CTU row at 1080p) has no
-  // in-frame CU: nothing is predicted, its tile is never read
-  const bool regionOut = tx0 + C::MARGIN >= W || ty0 + C::MARGIN >= H;
-  for (int dupS = 0; dupS < ((VAME_DUP & 8) ? 2 : 1) && !regionOut; dupS++) {
-    constexpr int CPR = C::TILE / 8;  // chunks per tile row
-    constexpr int NCH = C::TILE * CPR;
-    constexpr int PER = (NCH + C::THREADS - 1) / C::THREADS;
-    uint4 v[PER];
-#pragma unroll
-    for (int j = 0; j < PER; j++) {
-      const int ch = tid + j * C::THREADS;
-      if (ch < NCH) {
-        const int ty = ch / CPR, cx = (ch % CPR) * 8;
-        const int fy = clampi(ty0 + ty, 0, H - 1), fx = tx0 + cx;
-        const uint16_t* row = ref + (size_t)fy * W;
-        if (fx >= 0 && fx + 7 < W) {
-          v[j] = *reinterpret_cast<const uint4*>(row + fx);
-        } else {
-          unsigned a[8];
-#pragma unroll
-          for (int m = 0; m < 8; m++) a[m] = row[clampi(fx + m, 0, W - 1)];
-          v[j] = make_uint4(a[0] | (a[1] << 16), a[2] | (a[3] << 16), a[4] | (a[5] << 16),
-                            a[6] | (a[7] << 16));
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < PER; j++) {
-      const int ch = tid + j * C::THREADS;
-      if (ch < NCH) *reinterpret_cast<uint4*>(&s_tile[(ch / CPR) * C::TP + (ch % CPR) * 8]) = v[j];
-    }
-  }
-  __syncthreads();
-  PH_MARK(kPhStage)
-#endif
   if (!coop && wv >= nWaves) {  // wave-uniform: an autonomous wave without CUs
     PH_FLUSH
     return;
@@ -1667,19 +1342,12 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   const int sbTop = max(sbIdx - sbCols, 0), sbBot = min(sbIdx + sbCols, C::NSB - 1);
   const bool leader = myCu >= 0 && (lane & ((1 << logS) - 1)) == (1 << logS) - 1;
 
-#if VAME_PASS_T
-  // one copy of the pass per CP count: ncp is a compile-time constant in each,
-  // so the 2-CP pass carries none of the 3-CP selects and branches
+  // one copy of the pass per CP count and item class: ncp and coop are
+  // compile-time constants in each, so the 2-CP pass carries none of the 3-CP
+  // selects and branches, and each copy keeps its spills outside its loops
   auto run_pass = [&](auto ncpTag, auto coopTag) {
     constexpr int ncp = decltype(ncpTag)::value;
-#if VAME_PASS_T >= 2
-    constexpr bool coop = decltype(coopTag)::value;  // and per item class
-#endif
-#else
-  for (int pass = 0; pass < 2; pass++) {
-    const int ncp = pass == 0 ? 2 : 3;
-    if ((pass == 0 && !p.run2) || (pass == 1 && !p.run3)) continue;
-#endif
+    constexpr bool coop = decltype(coopTag)::value;
     const int niter = (ncp == 3 ? 4 : 5) + p.extra;
 
     // ---- per-CU initial CPMVs (2 CP: zero; 3 CP: derived from the 2-CP winner)
@@ -1726,9 +1394,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       }
       st.bestCost = (long long)costInit;
       st.satd = 0;
-#if VAME_RATE_UPD
       st.rate = affine_bits(c, ncp);
-#endif
       st.inframe = (cx + (1 << cs.lw) <= W) && (cy + (1 << cs.lh) <= H);
       st.live = st.inframe;
     }
@@ -1746,7 +1412,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       if (live && !(VAME_ABLATE & 8)) {
         Geo gp = g;
         int sxp = sx, syp = sy;
-        if (VAME_OPQ & 1) opaque_geo(gp, sxp, syp);
+        opaque_geo(gp, sxp, syp);  // recomputed per phase (not hoisted: VGPRs)
         int cp[6];
         for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
         const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
@@ -1781,34 +1447,16 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       PH_MARK(kPhPredict)
 
       // =============== cost, best update (affine.cl:416-457) ===============
-      // The rate (calc_affine_bits, aux_functions.cl:2140-2189) is spread over
-      // the CU's first lanes: lane j < 2 * nCP codes component j of the MVD
-      // against the zero predictor, three DPP steps sum them into the CU's
-      // lane 7, which forms the cost and keeps the strict best.
+      // The CU's lane 7 forms the cost from the SATD sum and the rate of the
+      // current CPMVs (calc_affine_bits, aux_functions.cl:2140-2189, kept in
+      // CuState by the update step) and keeps the strict best.
       const bool lastIter = iter == niter;
       {
-        int b = 0;
-        int cuR = myCu, locR = local;  // recomputed addresses (no loop-carried copies)
-        if (VAME_OPQ & 4) { opaque(cuR); opaque(locR); }
-        const CuState& sr = s_st[cuR < 0 ? 0 : cuR];
-        const bool rate = cuR >= 0 && (iter == 0 || sr.live);
-#if !VAME_RATE_UPD
-        if (rate && locR < 2 * ncp) {
-          int v = to_quarter(sr.cur[locR]);
-          if (locR >= 2) v -= to_quarter(sr.cur[locR & 1]);
-          b = eg_bits(v);
-        }
-        b += dpp32<0x111, 0xF>(b);  // row_shr:1, 2, 4: lane 7 of the CU sums lanes 0..7
-        b += dpp32<0x112, 0xF>(b);
-        b += dpp32<0x114, 0xF>(b);
-#endif
         int better = 0;
         if (myCu >= 0 && local == 7) {
           CuState& st = s_st[myCu];
-#if VAME_RATE_UPD
-          b = st.rate;
-#endif
-          if (rate) {
+          const int b = st.rate;
+          if (iter == 0 || st.live) {
             const float prod = __fmul_rn(pa.lambda, (float)(b + kRuiBits));
             const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
             if (cost < st.bestCost) {
@@ -1837,7 +1485,6 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           X[5] = ext_row(bt, dpp32<0x138, 0xF>((int)bt.y), dpp32<0x130, 0xF>((int)bt.x));
           Geo gg = g;
           int sxg = sx, syg = sy;
-          if (VAME_OPQ & 2) opaque_geo(gg, sxg, syg);
           grad_sb(sxg, syg, gg, X, Og, S);
           if (VAME_DUP & 2) {
             int S2[5];
@@ -1848,9 +1495,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           }
         }
         if (!(VAME_ABLATE & 4)) {
-          int cuV = myCu;
-          if (VAME_OPQ & 8) opaque(cuV);
-          long long* dst = s_val[cuV < 0 ? 0 : cuV];
+          long long* dst = s_val[myCu < 0 ? 0 : myCu];
           if (ncp == 2)
             reduce_equations<2>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
           else
@@ -1869,11 +1514,12 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       PH_MARK(kPhGradient)
 
       // =============== solve + CPMV update (affine.cl:782-893), per CU segment ===============
-      if (VAME_PRIO) __builtin_amdgcn_s_setprio(VAME_PRIO);
+      __builtin_amdgcn_s_setprio(kSolvePrio);
       if (!(VAME_ABLATE & 1)) {
         // the CU's lanes in its first wave solve it together
         int cuS = myCu, loc = local;
-        if (VAME_OPQ & 16) { opaque(cuS); opaque(loc); }
+        opaque(cuS);  // recomputed, not loop-carried (VGPRs)
+        opaque(loc);
         const bool solver = cuS >= 0 && loc < 64;
         const bool act = solver && s_st[cuS].live;
         const int Ls = 1 << logS;
@@ -1916,7 +1562,6 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             st.cur[j] = v;
             q = to_quarter(v);
           }
-#if VAME_RATE_UPD
           // the rate of the new CPMVs (calc_affine_bits, aux_functions.cl:2140-2189)
           // rides on the same lane sum: component j codes q_j - q_(j & 1) for
           // j >= 2 (RT - LT from lane j - 2, LB - LT from lane j - 4)
@@ -1924,7 +1569,6 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             const int q2 = dpp32<0x112, 0xF>(q), q4 = dpp32<0x114, 0xF>(q);
             if (loc < 2 * ncp) f += eg_bits(q - (loc >= 4 ? q4 : loc >= 2 ? q2 : 0)) << 8;
           }
-#endif
           f += dpp32<0x111, 0xF>(f);  // row_shr:1, 2, 4: lane 7 sums lanes 0..7
           f += dpp32<0x112, 0xF>(f);
           f += dpp32<0x114, 0xF>(f);
@@ -1932,19 +1576,17 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             // moved, and not back to the previous (flag fields: bits 0-3 and 4-7)
             liveNew = (f & 15) != 0 && ((f >> 4) & 15) != 0;
             st.live = liveNew;
-#if VAME_RATE_UPD
             st.rate = f >> 8;
-#endif
           }
         }
         if (!coop) {  // leave once every CU of this wave is settled (wave-local)
           if (__ballot(liveNew) == 0) {
-            if (VAME_PRIO) __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(0);
             break;
           }
         }
       }
-      if (VAME_PRIO) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
       phase_sync(coop);
       PH_MARK(kPhSolve)
       if (coop) {  // leave once every CU of the item is settled (flags read after the sync)
@@ -1971,9 +1613,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     }
     phase_sync(coop);
     PH_MARK(kPhTail)
-#if VAME_PASS_T
   };
-#if VAME_PASS_T >= 2
   if (coop) {
     if (p.run2) run_pass(std::integral_constant<int, 2>{}, std::true_type{});
     if (p.run3) run_pass(std::integral_constant<int, 3>{}, std::true_type{});
@@ -1981,20 +1621,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     if (p.run2) run_pass(std::integral_constant<int, 2>{}, std::false_type{});
     if (p.run3) run_pass(std::integral_constant<int, 3>{}, std::false_type{});
   }
-#else
-  if (p.run2) run_pass(std::integral_constant<int, 2>{}, std::false_type{});
-  if (p.run3) run_pass(std::integral_constant<int, 3>{}, std::false_type{});
-#endif
-#else
-  }
-#endif
   PH_FLUSH
 }
 
 // Distinct entry points so profiles tell the two work-item classes apart.
 // Quadrant items: 4 workgroups per CU fit the LDS (~35 KB each), so cap the
 // VGPRs at 128 to let all 16 waves be resident.
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VAME_WAVES))) void affine_me_quad(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad(
     KParams p) {
   affine_me_body<64, false>(p);
 }
@@ -2002,7 +1635,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VAME_W
 // per sub-block of a 128x128 CU.
 __global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_body<128, false>(p); }
 // The same with PROF (vame_set_prof).
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(VAME_WAVES))) void affine_me_quad_prof(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad_prof(
     KParams p) {
   affine_me_body<64, true>(p);
 }

@@ -76,6 +76,19 @@ class Engine:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    def _check_out(self, out, align: int):
+        """Caller-supplied result buffers must hold exactly the launch's rows:
+        int64 cost[n], int32 cpmv[n, 7], contiguous, on the engine's device."""
+        cost, cpmv = out
+        n = self.n_cus(align)
+        ok = (cost.dtype == torch.int64 and cost.numel() == n and cost.is_contiguous()
+              and cpmv.dtype == torch.int32 and tuple(cpmv.shape) == (n, 7) and cpmv.is_contiguous()
+              and cost.device == self.device and cpmv.device == self.device)
+        if not ok:
+            raise ValueError(f"result buffers must be int64[{n}] and int32[{n}, 7], contiguous, "
+                             f"on {self.device} (align={align})")
+        return cost, cpmv
+
     def alloc_result(self, align: int):
         n = self.n_cus(align)
         return (torch.empty(n, dtype=torch.int64, device=self.device),
@@ -84,9 +97,12 @@ class Engine:
     def affine_me(self, ref, cur, lam: float, align: int, ncp: int, extra: int = 0,
                   prev: torch.Tensor | None = None, out=None):
         ref, cur = self._frame(ref), self._frame(cur)
-        cost, cpmv = out if out is not None else self.alloc_result(align)
-        if ncp == 3 and (prev is None or prev.shape != (self.n_cus(align), 7)):
-            raise ValueError("3-CP needs prev = the same-alignment 2-CP cpmvs [n, 7]")
+        if align not in (0, 1) or ncp not in (2, 3):
+            raise ValueError("align must be 0/1 and ncp 2/3")
+        cost, cpmv = self._check_out(out, align) if out is not None else self.alloc_result(align)
+        if ncp == 3 and (prev is None or tuple(prev.shape) != (self.n_cus(align), 7)
+                         or prev.dtype != torch.int32 or prev.device != self.device):
+            raise ValueError("3-CP needs prev = the same-alignment 2-CP cpmvs, int32 [n, 7] on the device")
         check(lib().vame_affine_me(self._h, _ptr(ref), _ptr(cur), float(lam), align, ncp, extra,
                                    _ptr(prev.contiguous()) if prev is not None else None,
                                    _ptr(cost), _ptr(cpmv), self._stream()))
@@ -101,6 +117,17 @@ class Engine:
                 res[(r, name)] = self.alloc_result(m >> 1)
         return res
 
+    def _check_poc_out(self, out, nrefs: int, modes: int):
+        need = {(r, name) for r in range(nrefs) for m, name in enumerate(MODES)
+                if not ((m & 1) and not (modes & 2))}
+        missing = need - set(out)
+        if missing:
+            raise ValueError(f"result buffers missing for {sorted(missing)}")
+        for (r, name), bufs in out.items():
+            if r >= nrefs or name not in MODES:
+                raise ValueError(f"unexpected result key {(r, name)}")
+            self._check_out(bufs, MODES.index(name) >> 1)
+
     def affine_me_batch(self, jobs, modes: int = 3, extra: int = 0):
         """jobs: [(cur, refs, lam, out)] with out from alloc_poc; one
         vame_affine_me_batch call (32 (POC, refIdx) pairs per launch)."""
@@ -109,6 +136,7 @@ class Engine:
         for j, (cur, refs, lam, out) in enumerate(jobs):
             cur = self._frame(cur)
             refs = [self._frame(r) for r in refs]
+            self._check_poc_out(out, len(refs), modes)
             pr = PocResult()
             for (r, name), (cost, cpmv) in out.items():
                 m = MODES.index(name)
@@ -129,6 +157,7 @@ class Engine:
         cur = self._frame(cur)
         refs = [self._frame(r) for r in refs]
         out = out if out is not None else self.alloc_poc(len(refs), modes)
+        self._check_poc_out(out, len(refs), modes)
         pr = PocResult()
         for (r, name), (cost, cpmv) in out.items():
             m = MODES.index(name)

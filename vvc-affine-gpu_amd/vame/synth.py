@@ -5,6 +5,12 @@ Every value is built from integer hashing and +,-,*,/ on float64 only -- no
 transcendental numpy ufuncs -- so the same seed yields the same bytes on any
 x86 host (numpy's SIMD sin/cos dispatch differs between CPUs; these do not).
 
+This numpy code is the specification.  `synth_frame` / `synth_sequence` run
+the native generator (csrc/vame_synth.c, lib/libvame_synth.so: the same
+arithmetic in the same order, OpenMP over rows) when it is built -- a 240-frame
+3840x2160 sequence (BASELINE configs[4]) would take hours here -- and
+tests/test_synth.py checks both produce identical bytes.
+
 Layout matches the reference inputs (main.cpp:313-328): `orig[k]` is POC k+1
 (the frame being coded), `recon[k]` is the reconstructed POC k (the reference
 picture pool), each H x W uint16 in [0, 1023].
@@ -18,7 +24,9 @@ translation) so the affine search has something to find.
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 
 import numpy as np
 
@@ -88,12 +96,25 @@ def canvas(x: np.ndarray, y: np.ndarray, W: int, H: int, seed: int) -> np.ndarra
     return f
 
 
-def synth_frame(W: int, H: int, poc: int, seed: int = 0x5EED) -> np.ndarray:
-    """Original POC `poc` (H x W uint16)."""
-    zoom = 1.0 + 0.004 * poc
+def _pixel_noise(x: np.ndarray, y: np.ndarray, salt: int, amp: int) -> np.ndarray:
+    """Uniform integer in [-amp, amp] per pixel from a hash of (x, y, salt)."""
+    with np.errstate(over="ignore"):
+        h = (x.astype(np.int64).view(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+             + y.astype(np.int64).view(np.uint64) * np.uint64(0xC2B2AE3D27D4EB4F)
+             + np.uint64(salt & 0xFFFFFFFFFFFFFFFF))
+        h = _mix(h)
+    return (((h >> np.uint64(32)) * np.uint64(2 * amp + 1)) >> np.uint64(32)).astype(np.int64) - amp
+
+
+def camera(poc: int):
+    """Cumulative camera of POC `poc`: (zoom, cos, sin, tx, ty)."""
     ang = math.radians(0.15) * poc
-    ca, sa = math.cos(ang), math.sin(ang)
-    tx, ty = 1.25 * poc, -0.75 * poc
+    return 1.0 + 0.004 * poc, math.cos(ang), math.sin(ang), 1.25 * poc, -0.75 * poc
+
+
+def synth_frame_np(W: int, H: int, poc: int, seed: int = 0x5EED) -> np.ndarray:
+    """Original POC `poc` (H x W uint16) -- the numpy specification."""
+    zoom, ca, sa, tx, ty = camera(poc)
     yy, xx = np.meshgrid(np.arange(H, dtype=np.float64), np.arange(W, dtype=np.float64),
                          indexing="ij")
     cx, cy = W / 2.0, H / 2.0
@@ -103,8 +124,7 @@ def synth_frame(W: int, H: int, poc: int, seed: int = 0x5EED) -> np.ndarray:
     sx = ca * px + sa * py + cx
     sy = -sa * px + ca * py + cy
     f = canvas(sx, sy, W, H, seed)
-    rng = np.random.Generator(np.random.PCG64(seed * 1000003 + poc))
-    f = np.floor(f + 0.5) + rng.integers(-2, 3, size=f.shape)
+    f = np.floor(f + 0.5) + _pixel_noise(xx, yy, seed * 1000003 + poc, 2)
     return np.clip(f, 0, 1023).astype(np.uint16)
 
 
@@ -112,24 +132,97 @@ def recon_noise_amp(qp: int) -> int:
     return max(0, (qp - 17) // 5)
 
 
+def recon_np(frame: np.ndarray, poc: int, qp: int, seed: int = 0x5EED) -> np.ndarray:
+    """Reconstructed POC `poc` from its original -- the numpy specification."""
+    H, W = frame.shape
+    amp = recon_noise_amp(qp)
+    yy, xx = np.meshgrid(np.arange(H), np.arange(W), indexing="ij")
+    r = frame.astype(np.int64) + (_pixel_noise(xx, yy, (seed ^ 0xC0FFEE) * 7919 + poc, amp) if amp else 0)
+    return np.clip(r, 0, 1023).astype(np.uint16)
+
+
+_native = None
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
+                         "libvame_synth.so")
+
+
+def native():
+    """ctypes handle of lib/libvame_synth.so, or None when it is not built."""
+    global _native
+    if _native is None:
+        if not os.path.exists(_LIB_PATH) or os.environ.get("VAME_SYNTH_NUMPY"):
+            return None
+        L = ctypes.CDLL(_LIB_PATH)
+        I, D, P, U = ctypes.c_int, ctypes.c_double, ctypes.c_void_p, ctypes.c_uint64
+        L.vame_synth_frame.argtypes = [I, I, U, I, D, D, D, D, D, P]
+        L.vame_synth_frame.restype = None
+        L.vame_synth_recon.argtypes = [P, I, I, U, I, I, P]
+        L.vame_synth_recon.restype = None
+        L.vame_synth_write_csv.argtypes = [ctypes.c_char_p, P, I, I, I]
+        _native = L
+    return _native
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def synth_frame(W: int, H: int, poc: int, seed: int = 0x5EED) -> np.ndarray:
+    """Original POC `poc` (H x W uint16)."""
+    L = native()
+    if L is None:
+        return synth_frame_np(W, H, poc, seed)
+    out = np.empty((H, W), np.uint16)
+    L.vame_synth_frame(W, H, seed & 0xFFFFFFFFFFFFFFFF, poc, *camera(poc), _p(out))
+    return out
+
+
+def recon_frame(frame: np.ndarray, poc: int, qp: int, seed: int = 0x5EED) -> np.ndarray:
+    """Reconstructed POC `poc`: its original + uniform noise of +-floor((QP-17)/5)."""
+    L = native()
+    if L is None:
+        return recon_np(frame, poc, qp, seed)
+    H, W = frame.shape
+    frame = np.ascontiguousarray(frame, np.uint16)
+    out = np.empty((H, W), np.uint16)
+    L.vame_synth_recon(_p(frame), W, H, seed & 0xFFFFFFFFFFFFFFFF, poc, recon_noise_amp(qp), _p(out))
+    return out
+
+
 def synth_sequence(W: int, H: int, n_frames: int, qp: int = 32, seed: int = 0x5EED):
     """(orig, recon): orig[k] = POC k+1, recon[k] = reconstructed POC k; each
     (n_frames, H, W) uint16."""
-    frames = [synth_frame(W, H, poc, seed) for poc in range(n_frames + 1)]
-    orig = np.stack(frames[1:])
-    amp = recon_noise_amp(qp)
-    recon = []
+    orig = np.empty((n_frames, H, W), np.uint16)
+    recon = np.empty((n_frames, H, W), np.uint16)
+    prev = synth_frame(W, H, 0, seed)
     for poc in range(n_frames):
-        rng = np.random.Generator(np.random.PCG64((seed ^ 0xC0FFEE) * 7919 + poc))
-        r = frames[poc].astype(np.int32) + rng.integers(-amp, amp + 1, size=(H, W))
-        recon.append(np.clip(r, 0, 1023).astype(np.uint16))
-    return orig, np.stack(recon)
+        recon[poc] = recon_frame(prev, poc, qp, seed)
+        prev = synth_frame(W, H, poc + 1, seed)
+        orig[poc] = prev
+    return orig, recon
+
+
+def synth_pocs(W: int, H: int, pocs, ref_pocs, qp: int = 32, seed: int = 0x5EED):
+    """Only the frames a frame shard needs: {poc: orig POC} for `pocs` and
+    {poc: recon POC} for `ref_pocs` -- the same bytes as synth_sequence."""
+    orig = {p: synth_frame(W, H, p, seed) for p in pocs}
+    recon = {}
+    for p in ref_pocs:
+        f = orig[p] if p in orig else synth_frame(W, H, p, seed)
+        recon[p] = recon_frame(f, p, qp, seed)
+    return orig, recon
 
 
 def write_csv(path: str, frames: np.ndarray) -> None:
     """Reference CSV layout: one row per frame line, ',' separated, frames stacked
     vertically (main.cpp:313-328)."""
     n, H, W = frames.shape
+    L = native()
+    if L is not None:
+        fr = np.ascontiguousarray(frames, np.uint16)
+        if L.vame_synth_write_csv(path.encode(), _p(fr), n, W, H) != 0:
+            raise OSError(f"cannot write {path}")
+        return
     with open(path, "w") as f:
         for k in range(n):
             np.savetxt(f, frames[k], fmt="%d", delimiter=",")
