@@ -108,7 +108,9 @@ def test_2cp_only_mode(engines):
     assert set(out) == {(0, "FULL_2CP"), (0, "HALF_2CP")}
     for name in ("FULL_2CP", "HALF_2CP"):
         hc, hp = host(out[(0, name)])
-        np.testing.assert_array_equal(hc, z[name + "_cost"])
+        np.testing.assert_array_equal(hc, z[name + "_cost"], err_msg=name)
+        np.testing.assert_array_equal(cp6(hp), z[name + "_cpmv"], err_msg=name)
+        assert (hp[:, 0] == 2).all()
 
 
 REF_HARNESS = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle", "_ref", "ref_harness_hip")
@@ -214,15 +216,18 @@ def test_fused_vs_oracle_2160p(engines, frames_2160p, qp):
 
 
 def test_batch_equals_per_poc(engines):
-    """vame_affine_me_batch (several POCs in shared launches; 36 pairs cross the
-    32-pair launch limit) == one vame_affine_me_poc per POC == the oracle."""
+    """vame_affine_me_batch (several POCs in shared launches; the 12-POC
+    sequence's 42 pairs cross the 32-pair launch limit) == one
+    vame_affine_me_poc per POC == the oracle, with the reference's ring and
+    per-POC lambdas (QP32)."""
     from vame import synth
+    from vame.hostlogic import lambda_for_poc, ref_list
     o, r = synth.synth_sequence(416, 240, 12, 32, seed=0xBA7C)
     eng = engines(416, 240)
     jobs, singles = [], []
     for poc in range(1, 13):
-        refs = [dev(r[k]) for k in range(max(0, poc - 3), poc)][::-1]  # 1..3 refs
-        lam = 40.0 + poc
+        refs = [dev(r[k]) for k in ref_list(poc)]
+        lam = lambda_for_poc(32, poc)
         jobs.append((dev(o[poc - 1]), refs, lam, eng.alloc_poc(len(refs), 3)))
         singles.append(eng.affine_me_poc(dev(o[poc - 1]), refs, lam, modes=3))
     outs = eng.affine_me_batch(jobs, 3, 0)
@@ -233,10 +238,61 @@ def test_batch_equals_per_poc(engines):
             sc, sp = host(single[key])
             np.testing.assert_array_equal(hc, sc, err_msg=f"POC{poc} {key}")
             np.testing.assert_array_equal(hp, sp, err_msg=f"POC{poc} {key}")
-    want = O.affine_me_pair(r[11], o[11], 52.0)  # POC 12, refIdx 0 = recon 11
-    for name, key in MODES.items():
-        hc, hp = host(outs[11][(0, name)])
-        np.testing.assert_array_equal(hc, want[key][0], err_msg=name)
+    for poc, refidx in ((12, 0), (12, 2), (8, 3)):  # POC 12 ref 2 / POC 8 ref 3: long-term POC 8 / 0
+        rp = ref_list(poc)[refidx]
+        want = O.affine_me_pair(r[rp], o[poc - 1], lambda_for_poc(32, poc))
+        for name, key in MODES.items():
+            hc, hp = host(outs[poc - 1][(refidx, name)])
+            np.testing.assert_array_equal(hc, want[key][0], err_msg=f"POC{poc} ref{refidx} {name}")
+            np.testing.assert_array_equal(cp6(hp), oracle_cp6(want[key][1]),
+                                          err_msg=f"POC{poc} ref{refidx} {name}")
+
+
+def test_calls_keep_the_current_device(engines):
+    """The C-ABI entry points restore the caller's current device:
+    two engines used from one thread leave torch.cuda.current_device() alone."""
+    from vame.engine import Engine
+    ndev = torch.cuda.device_count()
+    devs = [0, 1] if ndev >= 2 else [0, 0]
+    engs = [Engine(416, 240, d) for d in devs]
+    try:
+        z = np.load(GOLDEN[0])
+        for cur_dev in sorted(set(devs)):
+            torch.cuda.set_device(cur_dev)
+            for e, d in zip(engs, devs):
+                ref = torch.from_numpy(z["ref"].view(np.int16)).to(f"cuda:{d}")
+                cur = torch.from_numpy(z["cur"].view(np.int16)).to(f"cuda:{d}")
+                e.affine_me_poc(cur, [ref], float(z["lam"]), modes=1)
+                assert torch.cuda.current_device() == cur_dev
+                e.set_timing(True)
+                e.get_timing(0)
+                assert torch.cuda.current_device() == cur_dev
+        torch.cuda.synchronize()
+    finally:
+        for e in engs:
+            e.close()
+        torch.cuda.set_device(0)
+
+
+def test_result_buffers_are_validated(engines):
+    """Wrong-size / wrong-dtype / wrong-device result buffers raise before any launch."""
+    z = np.load(GOLDEN[0])
+    eng = engines(int(z["W"]), int(z["H"]))
+    ref, cur = dev(z["ref"]), dev(z["cur"])
+    lam = float(z["lam"])
+    with pytest.raises(ValueError):
+        eng.affine_me(ref, cur, lam, 1, 2, out=eng.alloc_result(0))  # FULL rows for a HALF launch
+    c, p = eng.alloc_result(0)
+    with pytest.raises(ValueError):
+        eng.affine_me(ref, cur, lam, 0, 2, out=(c, p.to(torch.int64)))
+    with pytest.raises(ValueError):
+        eng.affine_me(ref, cur, lam, 0, 3, prev=p.to(torch.int64))
+    bad = eng.alloc_poc(1, 1)
+    bad[(0, "HALF_2CP")] = eng.alloc_result(0)
+    with pytest.raises(ValueError):
+        eng.affine_me_poc(cur, [ref], lam, modes=1, out=bad)
+    with pytest.raises(ValueError):
+        eng.affine_me_poc(cur, [ref], lam, modes=3, out=eng.alloc_poc(1, 1))  # 3-CP buffers missing
 
 
 @pytest.mark.parametrize("d", [(2, -3), (-4, 1)])
