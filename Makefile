@@ -36,6 +36,10 @@ ablate:
 variant:
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(LIBDIR)/libvame_$(NAME).so $(LIB_SRCS)
+# instrumentation build counting the sub-block predictions run: make count
+count:
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DVAME_COUNT_PRED=1 -shared -o $(LIBDIR)/libvame_count.so $(LIB_SRCS)
 # profiling-only build with per-phase shader-clock counters: make phase
 phase:
 	@mkdir -p $(LIBDIR)
@@ -63,4 +67,4 @@ clean:
 	rm -rf $(LIBDIR) $(BINDIR)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all lib cli synth oracle clean resource-usage ablate phase variant
+.PHONY: all lib cli synth oracle clean resource-usage ablate phase variant count

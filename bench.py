@@ -1,17 +1,26 @@
 #!/usr/bin/env python3
 """Throughput benchmark of the affine-ME hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4] [--qp QP]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+                    [--qp QP] [--frames F] [--no-cpu-baseline] [--no-spans]
 
 One step = the hot path over one batch of synthetic input: every (POC, refIdx)
-pair of the configuration's frames (refs from the reference's 4-slot list,
-lambda from its GOP-8 model), FULL + HALF candidate CUs, 2-CP (and 3-CP where
-the config asks for it), inputs resident in HBM.  Default = BASELINE.json
-configs[1]: 1920x1080 QP32, 2 frames, 2-CPMV affine only (3 pairs, 196,425
-candidate CUs per step).  Multi-GPU (torchrun, one rank per GPU): every rank
-codes its own frame shard (weak scaling) and the per-rank decision results are
-gathered to every rank with one RCCL all_gather per step (the decision-log
-gather of SURVEY.md §8e).  Rank 0 prints one JSON line.
+pair of this rank's POCs (refs from the reference's 4-slot ring, lambda from
+its GOP-8 model, main.cpp:578-707), FULL + HALF candidate CUs, 2-CP (and 3-CP
+where the config asks for it), inputs resident in HBM, in one
+vame_affine_me_batch call.  Default = BASELINE.json configs[1]: 1920x1080
+QP32, 2 frames, 2-CPMV affine only (3 pairs, 196,425 candidate CUs per step).
+
+Multi-GPU (torchrun, one rank per GPU): every rank codes the
+contiguous POC block shard.poc_shard(n, world, rank) of ONE sequence (the same
+synthetic seed on every rank), with no collective on the data path.
+  c2 / c3 / c4 scale weakly: the sequence has frames x N POCs, so every rank
+               codes about `frames` POCs (c2 at N = 1 is exactly configs[1]);
+  c5           scales strongly: 240 POCs of 3840x2160 in all (configs[4]).
+After the timed steps the decision records go to rank 0 in one RCCL gather
+(timed and reported separately as `gather`), and rank 0 recomputes the first
+and last POC of every rank's block and checks the gathered records byte for
+byte.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -28,14 +37,18 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 CONFIGS = {
-    "c2": dict(W=1920, H=1080, qp=32, frames=2, modes=1,
+    "c2": dict(W=1920, H=1080, qp=32, frames=2, modes=1, scaling="weak", steps=200, warmup=20,
                label="1920x1080 QP32, 2 frames, 2-CPMV affine only (FULL+HALF CUs)"),
-    "c3": dict(W=1920, H=1080, qp=32, frames=30, modes=3,
+    "c3": dict(W=1920, H=1080, qp=32, frames=30, modes=3, scaling="weak", steps=5, warmup=1,
                label="1920x1080 QP32, 30 frames, 2- and 3-CPMV affine (FULL+HALF CUs)"),
-    "c4": dict(W=3840, H=2160, qp=32, frames=30, modes=3,
+    "c4": dict(W=3840, H=2160, qp=32, frames=30, modes=3, scaling="weak", steps=3, warmup=1,
                label="3840x2160, 30 frames, 2- and 3-CPMV affine (FULL+HALF CUs)"),
+    "c5": dict(W=3840, H=2160, qp=32, frames=240, modes=3, scaling="strong", steps=2, warmup=1,
+               label="3840x2160 QP32, 240 frames frame-sharded over the GPUs, 2- and 3-CPMV "
+                     "affine (FULL+HALF CUs), gather of the decision records to rank 0"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+N_SIMD = 1024          # 256 CUs x 4 SIMDs
 
 
 def log(*a):
@@ -45,21 +58,19 @@ def log(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults: c2 steps are ~1 ms, so 200 timed steps after 20 warm-up steps
-    # (clocks settled) still take well under a second; c3 / c4 steps are
-    # 0.1 / 0.4 s
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--qp", type=int, default=None)
-    ap.add_argument("--frames", type=int, default=None)
+    ap.add_argument("--frames", type=int, default=None,
+                    help="sequence length (c5: total POCs; c2-c4: POCs per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-spans", action="store_true",
+                    help="skip the per-POC span step (profiling runs: identical launches only)")
     args = ap.parse_args()
-    if args.steps is None:
-        args.steps = 200 if args.config == "c2" else 5
-    if args.warmup is None:
-        args.warmup = 20 if args.config == "c2" else 1
     cfg = dict(CONFIGS[args.config])
+    args.steps = cfg["steps"] if args.steps is None else args.steps
+    args.warmup = cfg["warmup"] if args.warmup is None else args.warmup
     if args.qp is not None:
         cfg["qp"] = args.qp
     if args.frames is not None:
@@ -68,10 +79,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
     if world > 1:
         import torch.distributed as dist
-        # one rank per GPU; VAME_DIST_BACKEND=gloo rehearses the multi-rank path
-        # with several ranks on one GPU (the driver's runs use RCCL)
+        # one rank per GPU over RCCL; VAME_DIST_BACKEND=gloo rehearses the
+        # multi-rank path with several ranks on one GPU (the driver's runs use RCCL)
         backend = os.environ.get("VAME_DIST_BACKEND", "nccl")
         local = local % torch.cuda.device_count() if backend != "nccl" else local
         torch.cuda.set_device(local)
@@ -80,55 +92,35 @@ def main():
         else:
             dist.init_process_group(backend)
     else:
-        dist = None
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from vame import shard, synth
     from vame.engine import Engine
-    from vame.hostlogic import lambda_for_poc, ref_list
     from vame.metrics import pair_accounting
+    from vame.seqrun import ShardRun
 
-    W, H, qp, nf, modes = cfg["W"], cfg["H"], cfg["qp"], cfg["frames"], cfg["modes"]
+    W, H, qp, modes = cfg["W"], cfg["H"], cfg["qp"], cfg["modes"]
+    n_frames = cfg["frames"] * (world if cfg["scaling"] == "weak" else 1)
     ncps = (2, 3) if modes & 2 else (2,)
-    # this rank's frame shard (weak scaling: every rank codes nf frames of its own)
-    t0 = time.time()
-    orig, recon = synth.synth_sequence(W, H, nf, qp, seed=0x5EED + 7919 * rank)
-    log(f"[rank {rank}] synthesized {nf} frames {W}x{H} in {time.time() - t0:.1f}s")
-    d_orig = [torch.from_numpy(orig[k].view(np.int16)).to(dev) for k in range(nf)]
-    d_recon = [torch.from_numpy(recon[k].view(np.int16)).to(dev) for k in range(nf)]
     eng = Engine(W, H, dev.index)
-
-    plan = []  # (poc, refs, lambda, out buffers)
-    for poc in range(1, nf + 1):
-        refs = ref_list(poc)
-        plan.append((poc, refs, lambda_for_poc(qp, poc), eng.alloc_poc(len(refs), modes)))
-    n_pairs = sum(len(p[1]) for p in plan)
+    run = ShardRun(eng, W, H, qp, n_frames, modes, world, rank, dev)
+    log(f"[rank {rank}] POCs {run.pocs[:1]}..{run.pocs[-1:]} ({run.pairs} pairs) of {n_frames}, "
+        f"frames synthesized in {run.synth_s:.1f}s")
     acc = pair_accounting(W, H, ncps)
-    rows_per_step = n_pairs * acc["rows"]
+    rows_per_step = run.pairs * acc["rows"]
 
-    layout = [(len(refs), modes, (eng.n_cus(0), eng.n_cus(1))) for (_, refs, _, _) in plan]
-    words = shard.slab_words(layout)
-
-    # HIP events around every fused per-POC launch, on the stream it is issued
-    # on (the 128-class kernel runs on a side stream forked from and joined
-    # back into it): the hot path's span per launch
-    span_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in plan]
-    timing_spans = [False]
-
-    jobs = [(d_orig[poc - 1], [d_recon[r] for r in refs], lam, out) for (poc, refs, lam, out) in plan]
-
-    def step():
-        if timing_spans[0]:  # per-POC launches, each bracketed by events
-            for i, job in enumerate(jobs):
-                span_ev[i][0].record()
-                eng.affine_me_batch([job], modes, 0)
-                span_ev[i][1].record()
-        else:  # the step's POCs in shared launches (vame_affine_me_batch)
-            eng.affine_me_batch(jobs, modes, 0)
-        if dist is not None:  # the one exchange step: decision-log gather over RCCL/xGMI
-            shard.gather(shard.pack([pl[3] for pl in plan], words, dev), world)
+    # HIP events around every per-POC launch of one extra untimed step, on the
+    # stream it is issued on: the hot path's span per fused launch
+    def span_step():
+        ev = []
+        for job in run.jobs:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            eng.affine_me_batch([job], modes, 0)
+            b.record()
+            ev.append((a, b))
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev), len(ev)
 
     def barrier():
         torch.cuda.synchronize()
@@ -137,47 +129,50 @@ def main():
             torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        step()
+        run.step()
     barrier()
     eng.set_timing(True)
-    span_ms, span_n = 0.0, 0
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run.step()
     barrier()
     elapsed = time.perf_counter() - t_start
     quad_ms, quad_n = eng.get_timing(0)
     big_ms, big_n = eng.get_timing(1)
     eng.set_timing(False)
-    # one extra untimed step for the fused-launch spans (events on every launch)
-    timing_spans[0] = True
-    step()
-    torch.cuda.synchronize()
-    timing_spans[0] = False
-    for a, b in span_ev:
-        span_ms += a.elapsed_time(b)
-        span_n += 1
-    tmax = elapsed
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        tmax = float(t.item())
+    span_ms, span_n = (0.0, 0) if args.no_spans else span_step()
 
-    value = rows_per_step * world * args.steps / tmax
+    def all_reduce(vals, op):
+        if dist is None:
+            return vals
+        on = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor(vals, dtype=torch.float64, device=on)
+        dist.all_reduce(t, op=op)
+        return t.tolist()
+
+    ops = getattr(dist, "ReduceOp", None)
+    tmax = all_reduce([elapsed], ops and ops.MAX)[0]
+    rows_total = all_reduce([float(rows_per_step * args.steps)], ops and ops.SUM)[0]
+    value = rows_total / tmax
+
+    # the one exchange step, outside the timed steps: decision records to rank 0
+    barrier()
+    tg = time.perf_counter()
+    slabs, gather_bytes = run.gather()
+    torch.cuda.synchronize()
+    gather_ms = (time.perf_counter() - tg) * 1e3
+    gather_ms = all_reduce([gather_ms], ops and ops.MAX)[0]
+    check = run.verify(slabs) if rank == 0 else None
+    del slabs
+
     # roofline of the dominant kernel (quadrant work items, affine_me_quad)
-    quad_bytes = acc["bytes_quad"] * n_pairs * args.steps
+    quad_bytes = acc["bytes_quad"] * run.pairs * args.steps
     achieved = quad_bytes / (quad_ms * 1e-3) / 1e9 if quad_ms > 0 else 0.0
-    big_bytes = acc["bytes_big"] * n_pairs * args.steps
+    big_bytes = acc["bytes_big"] * run.pairs * args.steps
     big_achieved = big_bytes / (big_ms * 1e-3) / 1e9 if big_ms > 0 else 0.0
-    step_bytes = acc["bytes"] * n_pairs  # one step = every launch once
+    step_bytes = acc["bytes"] * run.pairs
     span_achieved = step_bytes / (span_ms * 1e-3) / 1e9 if span_ms > 0 else 0.0
-    traffic = None
-    pmc_path = os.path.join(REPO, "profiles", f"pmc_{args.config}.json")
-    if os.path.exists(pmc_path):
-        try:
-            traffic = json.load(open(pmc_path)).get("quad_hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    prof = load_profile(args.config, quad_ms / max(quad_n, 1))
 
     result = {
         "metric": "candidate CU-blocks/s at 1080p QP32; bit-exact CPMV/cost match vs reference",
@@ -188,34 +183,40 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": tmax * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": cfg["scaling"],
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
-        "config": {"workload": cfg["label"], "resolution": f"{W}x{H}", "qp": qp, "frames": nf,
-                   "pairs_per_step": n_pairs, "rows_per_step_per_gpu": rows_per_step,
-                   "modes": "2cp+3cp" if modes & 2 else "2cp", "parallelism": f"frame-shard x{world}"},
+        "config": {"workload": cfg["label"], "resolution": f"{W}x{H}", "qp": qp,
+                   "sequence_frames": n_frames, "pocs_rank0": len(run.pocs),
+                   "pairs_per_step_rank0": run.pairs, "rows_per_step_rank0": rows_per_step,
+                   "rows_per_step_all": rows_total / args.steps,
+                   "modes": "2cp+3cp" if modes & 2 else "2cp",
+                   "parallelism": f"frame-shard x{world} (poc_shard of one sequence)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": prof.get("traffic"),
                      "kernel": "affine_me_quad",
                      "avg_launch_ms": quad_ms / max(quad_n, 1),
                      "alg_bytes_per_launch": quad_bytes / max(quad_n, 1),
-                     "big_kernel_avg_launch_ms": big_ms / max(big_n, 1),
-                     # the 128-class kernel runs beside the quadrant kernel on a
-                     # side stream: its span is stretched by sharing the CUs
+                     # fraction of the algorithmic sub-block predictions the exact
+                     # early exit actually runs (instrumented build, profiles/)
+                     "executed_pred_frac": prof.get("executed_pred_frac"),
+                     # the kernel's real bound: VALU issue (rocprofv3 SQ counters, profiles/)
+                     "valu": prof.get("valu"),
                      "affine_me_ctu": {"achieved": big_achieved, "frac": big_achieved / HBM_PEAK_GBS,
                                        "avg_launch_ms": big_ms / max(big_n, 1),
                                        "alg_bytes_per_launch": big_bytes / max(big_n, 1)},
-                     # the whole hot path: one fused per-POC launch (both kernels)
                      "fused_poc_launch": {"achieved": span_achieved,
                                           "frac": span_achieved / HBM_PEAK_GBS,
                                           "avg_launch_ms": span_ms / max(span_n, 1),
                                           "alg_bytes_per_launch": step_bytes / max(span_n, 1)}},
+        "gather": {"to": "rank 0", "backend": "none" if dist is None else dist.get_backend(),
+                   "ms": gather_ms, "bytes_into_rank0": gather_bytes,
+                   "check": check},
     }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"], result["parity_sample"] = cpu_baseline(
-            orig, recon, plan, acc, ncps, W, H, modes)
+        result["cpu_baseline"], result["parity_sample"] = cpu_baseline(run, acc, ncps, W, H, modes)
     if dist is not None:
         dist.barrier()
     if rank == 0:
@@ -225,25 +226,85 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(orig, recon, plan, acc, ncps, W, H, modes, min_seconds=10.0):
-    """The CPU oracle (C restatement, OpenMP over the box's cores) on a bounded
-    sample of the same workload: the step's (POC, refIdx) pairs in order,
-    cycling until at least `min_seconds` of CPU work -- and a bit-exact check of
-    the GPU output of every pair it ran against it."""
+def load_profile(config: str, avg_launch_ms: float) -> dict:
+    """Counter-derived figures for the quadrant kernel from the committed
+    profile of this config (profiles/pmc_<config>.json, written by
+    profiles/pmc_summary.py from rocprofv3 passes over identical launches):
+      traffic             HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE)
+      valu                VALU issue: SQ_INSTS_VALU per launch over the SIMD
+                          cycles of this run's launch time at the profiled clock
+      executed_pred_frac  sub-block predictions run / algorithmic count"""
+    path = os.path.join(REPO, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return {}
+    p = json.load(open(path))
+    out = {"traffic": p.get("quad_hbm_bytes_per_launch"),
+           "executed_pred_frac": p.get("executed_pred_frac")}
+    sq = p.get("quad_sq")
+    if sq:
+        clk = sq["clock_ghz"]
+        cycles = avg_launch_ms * 1e-3 * clk * 1e9
+        rate = sq["insts_valu_per_launch"] / (N_SIMD * cycles)
+        out["valu"] = {"insts_valu_per_launch": sq["insts_valu_per_launch"],
+                       "issue_rate": rate, "peak_issue_rate": sq["peak_issue_rate"],
+                       "frac": rate / sq["peak_issue_rate"],
+                       "busy_frac_profiled": sq["valu_busy"],
+                       "clock_ghz_profiled": clk,
+                       "unit": "VALU wave-instructions per SIMD-cycle"}
+    return out
+
+
+def host_cpus():
+    """(threads the CPU baseline uses, description).  The baseline uses every
+    core this process may run on (sched affinity), capped by the cgroup CPU
+    quota and by OMP_NUM_THREADS where the host sets one (the GPU box gives
+    each GPU a 16-CPU share and sets OMP_NUM_THREADS=16)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    threads = min(x for x in (aff, quota, omp) if x)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, {"cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": aff,
+                     "cgroup_quota_cpus": quota, "omp_num_threads": omp}
+
+
+def cpu_baseline(run, acc, ncps, W, H, modes, min_seconds=10.0):
+    """The CPU oracle (C restatement, OpenMP) on a bounded sample of the same
+    workload: the step's (POC, refIdx) pairs in order, cycling until at least
+    `min_seconds` of CPU work -- and a bit-exact check of the GPU output of
+    every pair it ran against it."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_py as O
-    try:
-        threads = min(16, len(os.sched_getaffinity(0)))
-    except AttributeError:
-        threads = min(16, os.cpu_count() or 1)
-    pairs = [(poc, r, label, lam, out) for (poc, refs, lam, out) in plan
-             for r, label in enumerate(refs)]
+    from vame import synth
+    from vame.hostlogic import ref_list
+    threads, cpus = host_cpus()
+    orig, recon = synth.synth_pocs(W, H, run.pocs, sorted({p for q in run.pocs for p in ref_list(q)}),
+                                   run.qp, run.seed)
+    pairs = [(poc, r, rp, job[2], job[3]) for poc, job in zip(run.pocs, run.jobs)
+             for r, rp in enumerate(ref_list(poc))]
     names = (("FULL_2CP", (0, 2)), ("FULL_3CP", (0, 3)), ("HALF_2CP", (1, 2)), ("HALF_3CP", (1, 3)))
     rows, dt, ok, checked, k = 0, 0.0, True, set(), 0
     while dt < min_seconds or k == 0:
-        poc, r, label, lam, out = pairs[k % len(pairs)]
+        poc, r, rp, lam, out = pairs[k % len(pairs)]
         t0 = time.perf_counter()
-        res = O.affine_me_pair(recon[label], orig[poc - 1], lam, 0, modes=ncps, nthreads=threads)
+        res = O.affine_me_pair(recon[rp], orig[poc], lam, 0, modes=ncps, nthreads=threads)
         dt += time.perf_counter() - t0
         rows += acc["rows"]
         if (poc, r) not in checked:
@@ -260,7 +321,8 @@ def cpu_baseline(orig, recon, plan, acc, ncps, W, H, modes, min_seconds=10.0):
     base = {"value": rows / dt, "unit": "CU-blocks/s", "cores": threads, "kind": "port",
             "sample": f"{W}x{H}, {k} (POC, refIdx) pairs of the step's {len(pairs)} in order "
                       f"(cycled), FULL+HALF {'+'.join(f'{n}CP' for n in ncps)}, {rows} candidate "
-                      f"CUs, oracle/vame_oracle.c OpenMP x{threads}, {dt:.1f}s"}
+                      f"CUs, oracle/vame_oracle.c OpenMP x{threads}, {dt:.1f}s",
+            **cpus}
     return base, {"pairs": len(checked), "rows": len(checked) * acc["rows"], "bit_exact": ok}
 
 

@@ -87,8 +87,8 @@ def test_pair_accounting_matches_survey():
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
-@pytest.mark.parametrize("defs", [["-DVAME_ABLATE=63"], ["-DVAME_DUP=23"], ["-DVAME_PHASE_TIMING=1"]],
-                         ids=["ablate", "dup", "phase"])
+@pytest.mark.parametrize("defs", [["-DVAME_ABLATE=63"], ["-DVAME_DUP=23"], ["-DVAME_PHASE_TIMING=1"], ["-DVAME_COUNT_PRED=1"]],
+                         ids=["ablate", "dup", "phase", "count"])
 def test_instrumentation_builds_compile(tmp_path, defs):
     """The timing-only / profiling builds (make ablate / variant / phase; the
     only compile-time switches the kernel keeps) still compile for gfx950."""

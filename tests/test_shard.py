@@ -116,28 +116,25 @@ def test_two_rank_gather_equals_single_process(tmp_path):
 
 
 def gpu_worker(rank, world, port, outdir):
-    """One rank of the GPU frame-shard run: its POC block through the HIP engine
-    (vame_affine_me_batch on cuda:0 -- both ranks share the test box's one GPU),
-    compact records all_gathered over gloo."""
+    """One rank of the GPU frame-shard run, bench.py's path (vame/seqrun.py):
+    its POC block through the HIP engine (vame_affine_me_batch on cuda:0 --
+    both ranks share the test box's one GPU), the compact records gathered into
+    rank 0 over gloo, rank 0's sampled recompute check."""
     from vame.engine import Engine
+    from vame.seqrun import ShardRun
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    orig, recon = synth.synth_sequence(W, H, NF, QP, seed=7)
     dev = torch.device("cuda", 0)
     eng = Engine(W, H, 0)
-    mine = shard.poc_shard(NF, world, rank)
-    jobs = []
-    for p in mine:
-        refs = [torch.from_numpy(recon[r].view(np.int16)).to(dev) for r in ref_list(p)]
-        jobs.append((torch.from_numpy(orig[p - 1].view(np.int16)).to(dev), refs,
-                     lambda_for_poc(QP, p), eng.alloc_poc(len(refs), 1)))
-    outs = eng.affine_me_batch(jobs, 1, 0)
+    run = ShardRun(eng, W, H, QP, NF, 1, world, rank, dev, seed=7)
+    run.step()
     torch.cuda.synchronize()
-    words = max(shard.slab_words(layout(shard.poc_shard(NF, world, r))) for r in range(world))
-    slabs = shard.gather(shard.pack(outs, words, dev).cpu(), world)
+    slabs, _ = run.gather()
     if rank == 0:
+        check = run.verify(slabs)
+        assert check["byte_identical"], check
         allres = []
         for r in range(world):
             allres += shard.unpack(slabs[r], layout(shard.poc_shard(NF, world, r)))
@@ -165,3 +162,87 @@ def test_two_rank_gpu_shard_equals_oracle(tmp_path):
         for (r, m), (c, p) in want.items():
             gc, gp = g[f"{r}:{m}"]
             assert torch.equal(gc, c) and torch.equal(gp, p), (poc, r, m)
+
+
+class OracleEngine:
+    """CPU stand-in for vame.engine.Engine with the interface ShardRun uses
+    (n_cus, alloc_poc, affine_me_batch), computing with the oracle: runs the
+    bench's sequence-shard path (vame/seqrun.py) on CPU ranks."""
+
+    MODES = ("FULL_2CP", "FULL_3CP", "HALF_2CP", "HALF_3CP")
+
+    def __init__(self, W, H):
+        self.W, self.H = W, H
+        self.n_ctus = O.lib().vame_oracle_num_ctus(W, H)
+
+    def n_cus(self, align):
+        return self.n_ctus * (284 if align else 201)
+
+    def alloc_poc(self, nrefs, modes=3):
+        return {(r, m): (torch.empty(self.n_cus(k >> 1), dtype=torch.int64),
+                         torch.empty((self.n_cus(k >> 1), 7), dtype=torch.int32))
+                for r in range(nrefs) for k, m in enumerate(self.MODES) if not ((k & 1) and not modes & 2)}
+
+    def affine_me_batch(self, jobs, modes, extra):
+        for cur, refs, lam, out in jobs:
+            for r, ref in enumerate(refs):
+                res = O.affine_me_pair(ref.numpy().view(np.uint16), cur.numpy().view(np.uint16), lam,
+                                       extra, modes=(2, 3) if modes & 2 else (2,), nthreads=0)
+                for k, m in enumerate(self.MODES):
+                    if (r, m) in out:
+                        c, p = res[(k >> 1, 2 + (k & 1))]
+                        out[(r, m)][0].copy_(torch.from_numpy(c))
+                        out[(r, m)][1].copy_(torch.from_numpy(
+                            np.stack([p[f] for f in p.dtype.names], 1).astype(np.int32)))
+        return [j[3] for j in jobs]
+
+
+SEQ_W, SEQ_H, SEQ_N = 416, 240, 5  # 4x2 CTUs (last row 112 px high), POC 1..5 -> 11 pairs
+
+
+def bench_path_worker(rank, world, port, outdir):
+    """bench.py's multi-GPU path with the compute swapped for the oracle:
+    ShardRun over poc_shard of one sequence, step, gather to rank 0, rank 0's
+    recompute-and-compare check."""
+    from vame.seqrun import ShardRun
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    run = ShardRun(OracleEngine(SEQ_W, SEQ_H), SEQ_W, SEQ_H, 27, SEQ_N, 3, world, rank,
+                   torch.device("cpu"), seed=11)
+    run.step()
+    slabs, nbytes = run.gather()
+    if rank == 0:
+        check = run.verify(slabs)
+        torch.save({"slabs": slabs, "check": check, "bytes": nbytes, "pocs": run.pocs},
+                   os.path.join(outdir, "bench_path.pt"))
+    else:
+        assert slabs is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_bench_shard_path_two_ranks_equals_single_process(tmp_path):
+    """The exact sequence-shard path bench.py --gpus N runs (vame/seqrun.py:
+    one sequence, poc_shard per rank, one gather into rank 0, rank 0's sampled
+    recompute check), on 2 gloo ranks: the gathered records equal a 1-rank run
+    of the whole sequence word for word, and rank 0's own check passes."""
+    from vame.seqrun import ShardRun
+    port = free_port()
+    mp.spawn(bench_path_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    got = torch.load(os.path.join(tmp_path, "bench_path.pt"), weights_only=True)
+    assert got["check"]["byte_identical"] and len(got["check"]["pocs"]) >= 3
+    single = ShardRun(OracleEngine(SEQ_W, SEQ_H), SEQ_W, SEQ_H, 27, SEQ_N, 3, 1, 0,
+                      torch.device("cpu"), seed=11)
+    single.step()
+    whole = single.slab()
+    ofs = 0
+    for r in range(2):
+        pocs = shard.poc_shard(SEQ_N, 2, r)
+        n = shard.slab_words([(len(ref_list(p)), 3, (single.n_cus)) for p in pocs])
+        assert torch.equal(got["slabs"][r][:n], whole[ofs:ofs + n]), r
+        assert not got["slabs"][r][n:].any()  # zero padding to the largest shard
+        ofs += n
+    assert ofs == whole.numel()
+    assert got["bytes"] == 4 * got["slabs"][0].numel()

@@ -534,6 +534,19 @@ int vame_debug_phase_cycles(unsigned long long* out16, int reset) {
   return VAME_OK;
 }
 #endif
+#if VAME_COUNT_PRED
+// instrumentation builds: sub-block predictions run, [quad, ctu] (see vame_kernel.h)
+int vame_debug_pred_count(unsigned long long* out2, int reset) {
+  if (!out2) return VAME_E_INVALID;
+  VAME_HIP(hipDeviceSynchronize());
+  VAME_HIP(hipMemcpyFromSymbol(out2, HIP_SYMBOL(g_pred_count), sizeof(unsigned long long) * 2));
+  if (reset) {
+    unsigned long long z[2] = {};
+    VAME_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pred_count), z, sizeof(z)));
+  }
+  return VAME_OK;
+}
+#endif
 const char* vame_version(void) { return "vame 0.1 (gfx950)"; }
 
 }  // extern "C"

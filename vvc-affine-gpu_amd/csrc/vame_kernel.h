@@ -119,6 +119,23 @@ struct KParams {
 // the same).
 constexpr int kSolvePrio = 3;
 
+// VAME_COUNT_PRED (instrumentation builds, libvame_count.so): every lane counts
+// the sub-block predictions it runs (the exact early exit skips the rest of
+// the algorithmic n_pred per sub-block); g_pred_count[kernel: quad, ctu].
+#ifndef VAME_COUNT_PRED
+#define VAME_COUNT_PRED 0
+#endif
+#if VAME_COUNT_PRED
+__device__ unsigned long long g_pred_count[2];
+#define PC_DECL unsigned pc_n = 0;
+#define PC_ADD pc_n++;
+#define PC_FLUSH { if (pc_n) atomicAdd(&g_pred_count[REGION == 128], (unsigned long long)pc_n); }
+#else
+#define PC_DECL
+#define PC_ADD
+#define PC_FLUSH
+#endif
+
 // VAME_PHASE_TIMING (profiling-only builds, libvame_phase.so): every wave sums
 // the shader clock spent per phase and adds it to g_phase_cycles at exit.
 #ifndef VAME_PHASE_TIMING
@@ -1219,6 +1236,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   PH_DECL
+  PC_DECL
 
   // ---- XCD-aware block -> (ref, ctu, item): blocks b, b+8, ... share an XCD;
   // give each XCD a contiguous run of logical work (same CTUs -> L2 reuse).
@@ -1410,6 +1428,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       uint4 X[6];          // extended rows 0..3 (X[1..4]) and the neighbours' edges
       const bool live = active && s_st[myCu < 0 ? 0 : myCu].live;
       if (live && !(VAME_ABLATE & 8)) {
+        PC_ADD
         Geo gp = g;
         int sxp = sx, syp = sy;
         opaque_geo(gp, sxp, syp);  // recomputed per phase (not hoisted: VGPRs)
@@ -1622,6 +1641,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     if (p.run3) run_pass(std::integral_constant<int, 3>{}, std::false_type{});
   }
   PH_FLUSH
+  PC_FLUSH
 }
 
 // Distinct entry points so profiles tell the two work-item classes apart.

@@ -25,7 +25,15 @@
 //  * results are copied back asynchronously and the logs are formatted on the
 //    host while the GPU runs the next POC; stdout keeps the reference's order;
 //  * the OpenCL platform/device listing becomes a HIP device listing, and the
-//    per-PRED START/FINISH EXEC timestamps are not printed (PREDs are fused).
+//    per-PRED START/FINISH EXEC timestamps are not printed (PREDs are fused);
+//  * in the default fused mode one launch computes all four PREDs, so the
+//    reference's per-PRED *_EXEC keys carry the fused kernel time apportioned
+//    by each PRED's algorithmic work (sub-block predictions of its in-frame
+//    CUs, n_pred = 6 for 2 CP / 5 for 3 CP, + ExtraGradientIter); they sum to
+//    FUSED_POC_EXEC, the measured time.  --per-launch measures them directly;
+//  * extra keys after the reference's: READ_CSV_TIME (ingest), LOG_WRITE_TIME
+//    (host time formatting + writing the logs, overlapped with the GPU),
+//    LOG_BYTES.
 #include <hip/hip_runtime.h>
 #include <sys/time.h>
 #include <time.h>
@@ -213,6 +221,25 @@ int check_report(Cli& c) {
 }
 
 // main_aux_functions.h:59-68
+// Algorithmic work of one PRED of one (POC, ref) pair: sub-block predictions
+// over the in-frame CUs (affine.cl:192-193; n_pred 6 / 5 for 2 / 3 CP, + extra
+// iterations, affine.cl:172-177) -- the weights that apportion a fused
+// launch's kernel time to the reference's per-PRED keys.
+double pred_work(int W, int H, int align, int ncp, int extra) {
+  const int cols = (W + 127) / 128, rows = (H + 127) / 128;
+  double sb = 0;
+  int w, h, n, stride, xs[64], ys[64];
+  for (int g = 0; g < vame_num_groups(align); g++) {
+    if (vame_group_geometry(align, g, &w, &h, &n, &stride, xs, ys)) continue;
+    for (int ctu = 0; ctu < cols * rows; ctu++)
+      for (int k = 0; k < n; k++) {
+        const int x = (ctu % cols) * 128 + xs[k], y = (ctu / cols) * 128 + ys[k];
+        if (x + w <= W && y + h <= H) sb += (double)(w / 4) * (h / 4);
+      }
+  }
+  return sb * ((ncp == 2 ? 6 : 5) + extra);
+}
+
 void print_timestamp(const char* msg) {
   struct timeval tv;
   gettimeofday(&tv, nullptr);
@@ -606,11 +633,13 @@ int main(int argc, char** argv) {
     fclose(b);
   }
   print_timestamp("START READ .csv");
+  const double t_read0 = now_s();
   if (vame_read_frames(c.str("ReferenceFrames").c_str(), W, H, N, recon.data(), nthreads) ||
       vame_read_frames(c.str("OriginalFrames").c_str(), W, H, N, orig.data(), nthreads)) {
     printf("  [!] ERROR: could not read %d frames of %dx%d from the sample files\n", N, W, H);
     return 1;
   }
+  const double read_s = now_s() - t_read0;
   print_timestamp("FINISHED READ .csv");
 
   printf("Removing older outputs with identical names...\n");  // main.cpp:469 -> :1548
@@ -673,6 +702,7 @@ int main(int argc, char** argv) {
   // ---- writer: POCs in order (main.cpp:954-958 -> main_aux_functions.h:387-525)
   float pred_ns[4] = {0, 0, 0, 0}, fused_ns = 0;
   long long log_bytes = 0;
+  double log_s = 0;
   bool ok = true;
   for (int p = 1; p <= N && ok; p++) {
     Slab* s = nullptr;
@@ -701,9 +731,11 @@ int main(int argc, char** argv) {
             break;
           }
         }
+        const double tl = now_s();
         const long long nb =
             vame_log_append(prefix.c_str(), m, W, H, p, r, (const int64_t*)(s->host + L.off_cost[r][m]),
                             (const vame_cpmvs*)(s->host + L.off_cp[r][m]), nthreads);
+        log_s += now_s() - tl;
         if (nb < 0) {
           printf("  [!] ERROR: writing the log files %s_* failed\n", prefix.c_str());
           ok = false;
@@ -738,14 +770,25 @@ int main(int argc, char** argv) {
   // main_aux_functions.h:1416-1446 reportTimingResults (ns; float like the reference)
   printf("=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=\n");
   printf("TIMING RESULTS (nanoseconds)\n");
+  if (!per_launch) {  // fused launches: apportion by each PRED's algorithmic work
+    double wgt[4], sum = 0;
+    for (int m = 0; m < 4; m++) {
+      wgt[m] = ((m & 1) && !(mode_mask & VAME_MODE_3CP)) ? 0 : pred_work(W, H, m >> 1, (m & 1) ? 3 : 2, extra);
+      sum += wgt[m];
+    }
+    for (int m = 0; m < 4; m++) pred_ns[m] = (float)((double)fused_ns * wgt[m] / sum);
+  }
   printf("FULL_2CP_EXEC,%f\n", (double)pred_ns[0]);
   printf("FULL_3CP_EXEC,%f\n", (double)pred_ns[1]);
   printf("HALF_2CP_EXEC,%f\n", (double)pred_ns[2]);
   printf("HALF_3CP_EXEC,%f\n", (double)pred_ns[3]);
-  if (!per_launch) printf("FUSED_POC_EXEC,%f\n", (double)fused_ns);
-  printf("TOTAL_EXEC_TIME(%dx),%f\n", N,
-         (double)(pred_ns[0] + pred_ns[1] + pred_ns[2] + pred_ns[3] + fused_ns));
+  const double total_ns = per_launch ? (double)(pred_ns[0] + pred_ns[1] + pred_ns[2] + pred_ns[3])
+                                     : (double)fused_ns;
+  printf("TOTAL_EXEC_TIME(%dx),%f\n", N, total_ns);
   printf("OVERALL(%dx),%f\n", N, (double)(float)overall);
+  if (!per_launch) printf("FUSED_POC_EXEC,%f\n", (double)fused_ns);
+  printf("READ_CSV_TIME,%f\n", read_s * 1e9);
+  printf("LOG_WRITE_TIME,%f\n", log_s * 1e9);
   printf("LOG_BYTES,%lld\n", log_bytes);
   printf("=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=\n\n");
 

@@ -35,7 +35,8 @@ def cu_inventory(W: int, H: int):
 def pair_accounting(W: int, H: int, ncps=(2,), extra: int = 0):
     """Per (POC, ref) pair: rows, in-frame rows, and B_alg split by kernel class
     ('quad' = affine_me_quad items, 'big' = affine_me_ctu items)."""
-    acc = {"rows": 0, "rows_inframe": 0, "bytes_quad": 0, "bytes_big": 0, "sb_pred": 0}
+    acc = {"rows": 0, "rows_inframe": 0, "bytes_quad": 0, "bytes_big": 0, "sb_pred": 0,
+           "sb_pred_quad": 0, "sb_pred_big": 0}
     inv = cu_inventory(W, H)
     for ncp in ncps:
         npred = N_PRED[ncp] + extra
@@ -47,6 +48,7 @@ def pair_accounting(W: int, H: int, ncps=(2,), extra: int = 0):
                 nsb = (w // 4) * (h // 4)
                 b += npred * nsb * 162 + nsb * 32
                 acc["sb_pred"] += npred * nsb
+                acc["sb_pred_big" if big else "sb_pred_quad"] += npred * nsb
             acc["bytes_big" if big else "bytes_quad"] += b
     acc["bytes"] = acc["bytes_quad"] + acc["bytes_big"]
     return acc

@@ -106,8 +106,28 @@ def slab_words(layout: list[tuple[int, int, int]]) -> int:
     return w
 
 
+def poc_words(nrefs: int, modes: int, n_cus_per_align: tuple[int, int]) -> int:
+    """Words of one POC's records in a slab."""
+    return slab_words([(nrefs, modes, n_cus_per_align)])
+
+
+def gather_to_root(slab: torch.Tensor, world: int, root: int = 0, group=None):
+    """The one exchange step: every rank's equal-size slab to
+    `root` only (RCCL over xGMI on the GPU box: one ring-free gather into the
+    root, 1/world of an all_gather's traffic).  Returns the list of slabs on
+    the root, None elsewhere."""
+    import torch.distributed as dist
+    if world == 1:
+        return [slab]
+    rank = dist.get_rank(group)
+    dst = [torch.empty_like(slab) for _ in range(world)] if rank == root else None
+    dist.gather(slab, dst, dst=root, group=group)
+    return dst
+
+
 def gather(slab: torch.Tensor, world: int, group=None) -> list[torch.Tensor]:
-    """The one exchange step: every rank's slab to every rank (equal sizes)."""
+    """Every rank's slab to every rank (equal sizes) -- an all_gather, for
+    consumers that need the whole log on every rank."""
     import torch.distributed as dist
     if world == 1:
         return [slab]
