@@ -246,10 +246,19 @@ struct DeviceGuard {
     if (rc_) return rc_;   \
   } while (0)
 
-// (ctu, pair) blocks per template item, padded to a multiple of 8 (one per
-// XCD) so every item of a CTU lands on the same XCD (the kernel's item-major
-// block order; padding blocks exit at once)
-int combos(int n) { return (n + 7) / 8 * 8; }
+// Block order (affine_me_body): pairs in groups of about kGroupCombos (ctu,
+// pair) combinations -- the 3 pairs of a 1080p 2-frame step, whose tiles and
+// original samples the XCDs' L2s hold while every item of a CTU passes -- and
+// within a group, (ctu, pair) combinations per template item padded to a
+// multiple of 8 (one per XCD) so every item of a CTU lands on the same XCD
+// (padding blocks exit at once).  Returns the grid size.
+constexpr int kGroupCombos = 408;
+unsigned block_grid(KParams& k) {
+  k.groupPairs = std::max(1, std::min(k.nPairs, kGroupCombos / k.nCtus));
+  k.groupPer = (k.nCtus * k.groupPairs + 7) / 8 * 8;
+  const int groups = (k.nPairs + k.groupPairs - 1) / k.groupPairs;
+  return (unsigned)(groups * k.nItems * k.groupPer);
+}
 
 int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
            hipStream_t stream) {
@@ -273,7 +282,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     KParams kb = kp;
     kb.items = c->dBig;
     kb.nItems = c->nBig;
-    const unsigned grid = (unsigned)(kb.nItems * combos(kb.nCtus * kb.nPairs));
+    const unsigned grid = block_grid(kb);
     VAME_TRY(time_begin(c, 1, sBig));
     if (c->prof)
       hipLaunchKernelGGL(affine_me_ctu_prof, dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig, kb);
@@ -287,7 +296,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     KParams kq = kp;
     kq.items = quadFull ? c->dQuad : c->dQuad + c->nQuadFull;
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
-    const unsigned grid = (unsigned)(kq.nItems * combos(kq.nCtus * kq.nPairs));
+    const unsigned grid = block_grid(kq);
     VAME_TRY(time_begin(c, 0, sQuad));
     if (c->prof)
       hipLaunchKernelGGL(affine_me_quad_prof, dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad, kq);

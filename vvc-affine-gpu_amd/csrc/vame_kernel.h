@@ -93,6 +93,7 @@ struct KParams {
   const vame_cpmvs_dev* prev[2];  // [align]: 3-CP seeds when the 2-CP pass is not run
   const Item* items;
   int nItems, nCtus, nPairs;
+  int groupPairs, groupPer;  // pair groups of the block order (see affine_me_body)
   int W, H, ctusPerRow;
   int extra;
   int run2, run3;
@@ -109,7 +110,8 @@ struct KParams {
 #endif
 // VAME_DUP (timing-only builds, results stay correct): run a phase twice to
 // price it in throughput terms: bit 0 prediction, bit 1 gradient, bit 2
-// equation reduction, bit 4 the solve (on a copy of the system).
+// equation reduction, bit 4 the solve (on the system itself, before the real
+// one rebuilds it: no extra LDS); with bit 5 set, only in the 3-CP pass.
 #ifndef VAME_DUP
 #define VAME_DUP 0
 #endif
@@ -1224,7 +1226,6 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   __shared__ uint2 s_bot[C::NSB];  // row 3
   __shared__ __attribute__((aligned(16))) long long s_val[kMaxCu][kNumMom];
   __shared__ double s_mat[kMaxCu][42];  // per CU: N x (N + 1) system, N <= 6
-  __shared__ double s_mat_dup[(VAME_DUP & 16) ? kMaxCu : 1][42];
   __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
   __shared__ uint8_t s_eqmap[80];
   __shared__ CuState s_st[kMaxCu];
@@ -1238,21 +1239,23 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   PH_DECL
   PC_DECL
 
-  // ---- XCD-aware block -> (ref, ctu, item): blocks b, b+8, ... share an XCD;
-  // give each XCD a contiguous run of logical work (same CTUs -> L2 reuse).
-  // Item-major dispatch order: all (ctu, pair) blocks of template item 0
-  // first, then item 1, ...; the host lists the costlier items first, so the
-  // tail is made of short workgroups.  The host pads the (ctu, pair)
-  // combinations of an item to a multiple of 8, so combination j runs on XCD
-  // j % 8 (blocks are dealt round-robin over the 8 XCDs) for every item: the
-  // items of one CTU re-read its reference tile from the same L2.
+  // ---- XCD-aware block -> (pair group, item, ctu, pair).  The launch's pairs
+  // are taken in groups of groupPairs (about 400 (ctu, pair) combinations, a
+  // working set the XCDs' L2s hold); within a group the order is item-major:
+  // all (ctu, pair) blocks of template item 0 first, then item 1, ...; the
+  // host lists the costlier items first, so the tail is made of short
+  // workgroups.  The host pads a group's combinations to a multiple of 8
+  // (groupPer), so combination j runs on XCD j % 8 (blocks are dealt
+  // round-robin over the 8 XCDs) for every item: the items of one CTU re-read
+  // its reference tile and original samples from the same L2.
   const int b = blockIdx.x;
-  const int per = (int)gridDim.x / p.nItems;
-  const int itemIdx = b / per;
-  const int rest = b % per;
-  if (rest >= p.nCtus * p.nPairs) return;  // padding block (uniform, before any barrier)
+  const int gsz = p.nItems * p.groupPer;
+  const int grp = b / gsz, gr = b % gsz;
+  const int itemIdx = gr / p.groupPer;
+  const int rest = gr % p.groupPer;
+  const int pairIdx = grp * p.groupPairs + rest / p.nCtus;  // (POC, refIdx) pair of this launch
+  if (rest >= p.nCtus * p.groupPairs || pairIdx >= p.nPairs) return;  // padding (uniform, before any barrier)
   const int ctu = rest % p.nCtus;
-  const int pairIdx = rest / p.nCtus;  // (POC, refIdx) pair of this launch
   const PairArgs& pa = p.pair[pairIdx];
   const Item* it = p.items + itemIdx;
   const uint16_t* __restrict__ ref = pa.ref;
@@ -1366,6 +1369,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   auto run_pass = [&](auto ncpTag, auto coopTag) {
     constexpr int ncp = decltype(ncpTag)::value;
     constexpr bool coop = decltype(coopTag)::value;
+    constexpr int kDup = (VAME_DUP & 32) && ncp != 3 ? 0 : VAME_DUP;  // timing-only builds
     const int niter = (ncp == 3 ? 4 : 5) + p.extra;
 
     // ---- per-CU initial CPMVs (2 CP: zero; 3 CP: derived from the 2-CP winner)
@@ -1437,7 +1441,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
         const int satdLane = predict_sb<C::TILE, C::TP, PROF>(f, sxp, syp, gp, s_tile, tx0, ty0, ref, cur,
                                                         W, H, s_coef, Pr, Og);
-        if (VAME_DUP & 1) {
+        if (kDup & 1) {
           MvField f2 = f;
           opaque(f2.bx);
           uint2 P2[4], O2[4];
@@ -1505,7 +1509,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           Geo gg = g;
           int sxg = sx, syg = sy;
           grad_sb(sxg, syg, gg, X, Og, S);
-          if (VAME_DUP & 2) {
+          if (kDup & 2) {
             int S2[5];
             int sxd = sxg;
             opaque(sxd);
@@ -1519,7 +1523,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             reduce_equations<2>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
           else
             reduce_equations<3>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
-          if constexpr ((VAME_DUP & 4) != 0) {
+          if constexpr ((kDup & 4) != 0) {
             int ud = sx + 2;
             opaque(ud);
             if (ncp == 2)
@@ -1546,9 +1550,11 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         long long* V = s_val[cuS < 0 ? 0 : cuS];
         double* M = s_mat[cuS < 0 ? 0 : cuS];
         const CuSlot cs = s_cu[cuS < 0 ? 0 : cuS];
-        if constexpr ((VAME_DUP & 16) != 0) {  // timing-only: a throw-away solve first
+        if constexpr ((kDup & 16) != 0) {  // timing-only: a throw-away solve first
+          // on M itself, keeping V: the real solve below rebuilds M from V (no
+          // extra LDS, so the occupancy is the product build's)
           double dd2[6] = {0, 0, 0, 0, 0, 0};
-          double* M2 = s_mat_dup[cuS < 0 ? 0 : cuS];
+          double* M2 = M;
           if (ncp == 3)
             seg_solve<3, true>(V, M2, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd2);
           else
