@@ -84,8 +84,17 @@ def test_cli_logs_byte_identical_416(seq416):
     assert len(lines) == 1 + 2 + 3 + 4 + 4 + 4
     assert stdout.count("Reporting results POC=") == 4 * len(lines)
     for key in ("TIMING RESULTS (nanoseconds)", "FULL_2CP_EXEC,", "TOTAL_EXEC_TIME(6x),",
-                "OVERALL(6x),", "Writing headers", "FINISH HOST"):
+                "OVERALL(6x),", "Writing headers", "FINISH HOST", "READ_CSV_TIME,", "LOG_WRITE_TIME,"):
         assert key in stdout, key
+    # fused launches: the reference's per-PRED keys carry the fused kernel time
+    # apportioned by algorithmic work -- all non-zero, summing to FUSED_POC_EXEC
+    t = {l.split(",")[0]: float(l.split(",")[1]) for l in stdout.splitlines()
+         if l.count(",") == 1 and l.split(",")[1].replace(".", "").isdigit()}
+    preds = [t[k] for k in ("FULL_2CP_EXEC", "FULL_3CP_EXEC", "HALF_2CP_EXEC", "HALF_3CP_EXEC")]
+    assert all(v > 0 for v in preds)
+    assert abs(sum(preds) - t["FUSED_POC_EXEC"]) <= 1e-3 * t["FUSED_POC_EXEC"] + 4
+    assert t["TOTAL_EXEC_TIME(6x)"] == t["FUSED_POC_EXEC"]
+    assert preds[0] > preds[1] and preds[2] > preds[3]  # 6 vs 5 predictions per iteration set
 
 
 def test_cli_per_launch_and_two_workers_identical(seq416):
