@@ -260,6 +260,20 @@ unsigned block_grid(KParams& k) {
   return (unsigned)(groups * k.nItems * k.groupPer);
 }
 
+// The kernel instance of a launch mode (vame_kernel.h MODE: 1 = 2-CP only,
+// 2 = 3-CP only, 3 = 2-CP then 3-CP).
+using KernelFn = void (*)(KParams);
+template <bool BIG>
+KernelFn kernel_for(bool prof, int mode) {
+  if constexpr (BIG) {
+    if (prof) return mode == 1 ? affine_me_ctu_prof<1> : mode == 2 ? affine_me_ctu_prof<2> : affine_me_ctu_prof<3>;
+    return mode == 1 ? affine_me_ctu<1> : mode == 2 ? affine_me_ctu<2> : affine_me_ctu<3>;
+  } else {
+    if (prof) return mode == 1 ? affine_me_quad_prof<1> : mode == 2 ? affine_me_quad_prof<2> : affine_me_quad_prof<3>;
+    return mode == 1 ? affine_me_quad<1> : mode == 2 ? affine_me_quad<2> : affine_me_quad<3>;
+  }
+}
+
 int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
            hipStream_t stream) {
   // 128-class items (big LDS, 1 workgroup per CU) and quadrant items run on
@@ -271,6 +285,8 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
   // (batched c2 step 1.32 -> 1.245 ms).
   if (VAME_ABLATE & 16) bigItems = false;  // timing-only builds
   if (VAME_ABLATE & 32) quadFull = quadHalf = false;
+  const int mode = (kp.run2 ? 1 : 0) | (kp.run3 ? 2 : 0);  // the kernel instance (MODE)
+  if (mode == 0) return VAME_OK;
   const bool fork = bigItems && (quadFull || quadHalf);
   hipStream_t sBig = stream, sQuad = stream;
   if (fork) {
@@ -284,10 +300,8 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     kb.nItems = c->nBig;
     const unsigned grid = block_grid(kb);
     VAME_TRY(time_begin(c, 1, sBig));
-    if (c->prof)
-      hipLaunchKernelGGL(affine_me_ctu_prof, dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig, kb);
-    else
-      hipLaunchKernelGGL(affine_me_ctu, dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig, kb);
+    hipLaunchKernelGGL(kernel_for<true>(c->prof, mode), dim3(grid),
+                       dim3(Cfg<128>::THREADS), 0, sBig, kb);
     VAME_HIP(hipGetLastError());
     VAME_TRY(time_end(c, 1, sBig));
     return VAME_OK;
@@ -298,10 +312,8 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
     const unsigned grid = block_grid(kq);
     VAME_TRY(time_begin(c, 0, sQuad));
-    if (c->prof)
-      hipLaunchKernelGGL(affine_me_quad_prof, dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad, kq);
-    else
-      hipLaunchKernelGGL(affine_me_quad, dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad, kq);
+    hipLaunchKernelGGL(kernel_for<false>(c->prof, mode), dim3(grid),
+                       dim3(Cfg<64>::THREADS), 0, sQuad, kq);
     VAME_HIP(hipGetLastError());
     VAME_TRY(time_end(c, 0, sQuad));
     return VAME_OK;

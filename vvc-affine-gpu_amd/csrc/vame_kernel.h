@@ -922,10 +922,15 @@ struct CuState {
   int32_t prev[6];  // the CPMVs of the previous iteration (period-2 cycle test)
   int32_t best[6];
   int64_t bestCost;
+  int64_t bestCostSnap;  // bestCost as of the iteration's start (read by every lane of the CU)
   int32_t satd;
   int32_t inframe;
   int32_t live;
-  int32_t rate;  // calc_affine_bits of cur (set at init and by the update)
+  int32_t rate;      // calc_affine_bits of cur (set at init and by the update)
+  int32_t bestSatd;  // 2-CP pass: SATD of the best CPMVs
+  int32_t bestHasS;  // 2-CP pass: the best CPMVs' gradient sums are in s_bestS
+  int32_t seedSkip;  // 3-CP pass: iteration 0 reuses the 2-CP winner's prediction
+  int32_t pad;
 };
 
 template <int REGION>
@@ -1217,13 +1222,23 @@ __device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v
 }
 
 
-template <int REGION, bool PROF>
+// MODE (one kernel per launch mode, so each holds only the pass copies it
+// runs): 1 = 2-CP only, 2 = 3-CP only (seeds from p.prev), 3 = 2-CP then 3-CP.
+template <int REGION, bool PROF, int MODE>
 __device__ __forceinline__ void affine_me_body(const KParams& p) {
+  constexpr bool run2 = (MODE & 1) != 0, run3 = (MODE & 2) != 0;
   using C = Cfg<REGION>;
   __shared__ __attribute__((aligned(16))) uint16_t s_tile[C::TILE_ELEMS];
   static_assert((C::TP * 2) % 16 == 0 && C::TILE % 8 == 0, "16-byte tile rows");
   __shared__ uint2 s_top[C::NSB];  // row 0 of every sub-block's prediction (packed pairs)
   __shared__ uint2 s_bot[C::NSB];  // row 3
+  // the five gradient sums of every sub-block at its CU's best 2-CP iteration
+  // (3-CP seed reuse, see the 3-CP init)
+#ifdef VAME_EXP_NOBESTS
+  __shared__ int s_bestS[5][1];
+#else
+  __shared__ int s_bestS[5][C::NSB];
+#endif
   __shared__ __attribute__((aligned(16))) long long s_val[kMaxCu][kNumMom];
   __shared__ double s_mat[kMaxCu][42];  // per CU: N x (N + 1) system, N <= 6
   __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
@@ -1366,9 +1381,10 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   // one copy of the pass per CP count and item class: ncp and coop are
   // compile-time constants in each, so the 2-CP pass carries none of the 3-CP
   // selects and branches, and each copy keeps its spills outside its loops
-  auto run_pass = [&](auto ncpTag, auto coopTag) {
+  auto run_pass = [&](auto ncpTag, auto coopTag, auto keepTag) {
     constexpr int ncp = decltype(ncpTag)::value;
     constexpr bool coop = decltype(coopTag)::value;
+    constexpr bool keepS = decltype(keepTag)::value;  // 2-CP pass that feeds a 3-CP pass
     constexpr int kDup = (VAME_DUP & 32) && ncp != 3 ? 0 : VAME_DUP;  // timing-only builds
     const int niter = (ncp == 3 ? 4 : 5) + p.extra;
 
@@ -1383,7 +1399,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       int c[6] = {0, 0, 0, 0, 0, 0};
       if (ncp == 3) {
         int prev[4];
-        if (p.run2) {
+        if (run2) {
           for (int i = 0; i < 4; i++) prev[i] = st.best[i];
         } else {
           const vame_cpmvs_dev& pv =
@@ -1402,6 +1418,27 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         lby = shl(to_quarter(lby), 2);
         clip_mv(lbx, lby, cx, cy, W, H);
         c[0] = prev[0]; c[1] = prev[1]; c[2] = prev[2]; c[3] = prev[3]; c[4] = lbx; c[5] = lby;
+        // Seed reuse (exact): when the derived LB reproduces the 2-CP motion
+        // field -- (LB - LT) << (7 - log2 h) == (-(RT - LT).y, (RT - LT).x)
+        // << (7 - log2 w), i.e. no rounding or clipping in the derivation
+        // (always so for square CUs) -- iteration 0's MV field, spread test,
+        // prediction and gradients are those of the 2-CP winner, whose SATD
+        // and per-sub-block gradient sums the 2-CP pass kept.  Iteration 0
+        // then only re-prices the rate and rebuilds the 6-parameter equations.
+        int skip = 0, satd0 = 0;
+        if (run2 && st.bestHasS) {
+          const int hx = shl(prev[2] - prev[0], 7 - cs.lw), hy = shl(prev[3] - prev[1], 7 - cs.lw);
+          const int vx = shl(lbx - prev[0], 7 - cs.lh), vy = shl(lby - prev[1], 7 - cs.lh);
+          if (vx == -hy && vy == hx) {
+            skip = 1;
+            satd0 = st.bestSatd;
+          }
+        }
+        st.seedSkip = skip;
+        st.satd = satd0;
+      } else {
+        st.satd = 0;
+        st.bestHasS = 0;
       }
       // fresh constants (opaque): as loop-carried values the compiler kept
       // them in spill slots, whose scratch traffic reached HBM
@@ -1415,7 +1452,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         st.best[i] = c[i];
       }
       st.bestCost = (long long)costInit;
-      st.satd = 0;
+      st.bestCostSnap = (long long)costInit;
       st.rate = affine_bits(c, ncp);
       st.inframe = (cx + (1 << cs.lw) <= W) && (cy + (1 << cs.lh) <= H);
       st.live = st.inframe;
@@ -1431,7 +1468,10 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       uint2 Pr[4], Og[4];  // this lane's prediction and original rows (packed pairs)
       uint4 X[6];          // extended rows 0..3 (X[1..4]) and the neighbours' edges
       const bool live = active && s_st[myCu < 0 ? 0 : myCu].live;
-      if (live && !(VAME_ABLATE & 8)) {
+      // 3-CP iteration 0 of a seed-reuse CU: SATD (set at init) and gradient
+      // sums come from the 2-CP pass
+      const bool reuse = ncp == 3 && iter == 0 && s_st[myCu < 0 ? 0 : myCu].seedSkip;
+      if (live && !reuse && !(VAME_ABLATE & 8)) {
         PC_ADD
         Geo gp = g;
         int sxp = sx, syp = sy;
@@ -1470,27 +1510,49 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       PH_MARK(kPhPredict)
 
       // =============== cost, best update (affine.cl:416-457) ===============
-      // The CU's lane 7 forms the cost from the SATD sum and the rate of the
-      // current CPMVs (calc_affine_bits, aux_functions.cl:2140-2189, kept in
-      // CuState by the update step) and keeps the strict best.
+      // The cost is the SATD sum plus floor(lambda * (bits + 2)), the rate
+      // bits of the current CPMVs (calc_affine_bits, aux_functions.cl:2140-
+      // 2189) kept in CuState by the update step; the strict best is kept.
       const bool lastIter = iter == niter;
-      {
-        int better = 0;
+      bool better = false;  // keepS: this lane's CU improved
+      if constexpr (!keepS) {
+        // the CU's lane 7 prices and keeps the best; lanes 0-5 copy the CPMVs
+        int bet = 0;
         if (myCu >= 0 && local == 7) {
           CuState& st = s_st[myCu];
-          const int b = st.rate;
           if (iter == 0 || st.live) {
-            const float prod = __fmul_rn(pa.lambda, (float)(b + kRuiBits));
+            const float prod = __fmul_rn(pa.lambda, (float)(st.rate + kRuiBits));
             const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
             if (cost < st.bestCost) {
               st.bestCost = cost;
-              better = 1;
+              bet = 1;
             }
           }
           st.satd = 0;
         }
-        better = __builtin_amdgcn_update_dpp(0, better, 0x157, 0xF, 0xF, false);  // row_newbcast:7
-        if (myCu >= 0 && local < 6 && better) s_st[myCu].best[local] = s_st[myCu].cur[local];
+        bet = __builtin_amdgcn_update_dpp(0, bet, 0x157, 0xF, 0xF, false);  // row_newbcast:7
+        if (myCu >= 0 && local < 6 && bet) s_st[myCu].best[local] = s_st[myCu].cur[local];
+      } else {
+        // 2-CP pass followed by a 3-CP pass: every lane of the CU prices it, so
+        // each knows whether its CU improved and keeps its gradient sums for
+        // the 3-CP seed reuse.  The comparison is against the best cost as of
+        // the iteration's start: autonomous items read bestCost (the CU's
+        // lanes are one wave, whose LDS reads precede lane 7's write);
+        // cooperative items read bestCostSnap, refreshed in the solve phase.
+        if (myCu >= 0) {
+          CuState& st = s_st[myCu];
+          if (iter == 0 || st.live) {
+            const float prod = __fmul_rn(pa.lambda, (float)(st.rate + kRuiBits));
+            const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
+            better = cost < (coop ? st.bestCostSnap : st.bestCost);
+            if (better && local == 7) {
+              st.bestCost = cost;
+              st.bestSatd = st.satd;
+              st.bestHasS = !lastIter && st.live;  // its gradient sums follow in this iteration
+            }
+          }
+          if (local < 6 && better) st.best[local] = st.cur[local];
+        }
       }
       PH_MARK(kPhCost)
       if (lastIter) {  // uniform; the results below are written by other lanes
@@ -1501,7 +1563,10 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       // =============== gradients + normal equations (affine.cl:477-752) ===============
       {
         int S[5] = {0, 0, 0, 0, 0};
-        if (live && !(VAME_ABLATE & 2)) {
+        if (reuse && live) {
+#pragma unroll
+          for (int k = 0; k < 5; k++) S[k] = s_bestS[k][sbIdx];
+        } else if (live && !(VAME_ABLATE & 2)) {
           // the neighbours' edge rows, extended by the left / right lanes' copies
           const uint2 tb = s_bot[sbTop], bt = s_top[sbBot];
           X[0] = ext_row(tb, dpp32<0x138, 0xF>((int)tb.y), dpp32<0x130, 0xF>((int)tb.x));
@@ -1515,6 +1580,10 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             opaque(sxd);
             grad_sb(sxd, syg, gg, X, Og, S2);
             asm volatile("" ::"v"(S2[0] ^ S2[1] ^ S2[2] ^ S2[3] ^ S2[4]));
+          }
+          if (keepS && better) {  // the best iteration's sums, for the 3-CP seed reuse
+#pragma unroll
+            for (int k = 0; k < 5; k++) s_bestS[k][sbIdx] = S[k];
           }
         }
         if (!(VAME_ABLATE & 4)) {
@@ -1570,6 +1639,11 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         // CU applies scaleDeltaMvs to its delta (LT=(d0,d2), RT=(d1,d3),
         // LB=(d4,d5)), clampCpmvs and clipCpmvs, and the CU's lane 7 sums
         // the moved / cycle flags (DPP) into the CU's `live`
+        if (keepS && coop && solver && loc == 7) {  // the next cost phase's view; fresh SATD sums
+          CuState& st = s_st[cuS];
+          st.bestCostSnap = st.bestCost;
+          st.satd = 0;
+        }
         bool liveNew = false;
         if (act && loc < 8) {
           CuState& st = s_st[cuS];
@@ -1639,32 +1713,42 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     phase_sync(coop);
     PH_MARK(kPhTail)
   };
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using T = std::true_type;
+  using F = std::false_type;
+  // keepS: the 2-CP pass feeds a 3-CP pass (seed reuse)
+  using KeepS = std::integral_constant<bool, run3>;
   if (coop) {
-    if (p.run2) run_pass(std::integral_constant<int, 2>{}, std::true_type{});
-    if (p.run3) run_pass(std::integral_constant<int, 3>{}, std::true_type{});
+    if constexpr (run2) run_pass(I2{}, T{}, KeepS{});
+    if constexpr (run3) run_pass(I3{}, T{}, F{});
   } else {
-    if (p.run2) run_pass(std::integral_constant<int, 2>{}, std::false_type{});
-    if (p.run3) run_pass(std::integral_constant<int, 3>{}, std::false_type{});
+    if constexpr (run2) run_pass(I2{}, F{}, KeepS{});
+    if constexpr (run3) run_pass(I3{}, F{}, F{});
   }
   PH_FLUSH
   PC_FLUSH
 }
 
 // Distinct entry points so profiles tell the two work-item classes apart.
-// Quadrant items: 4 workgroups per CU fit the LDS (~35 KB each), so cap the
+// Quadrant items: 4 workgroups per CU fit the LDS (~40 KB each), so cap the
 // VGPRs at 128 to let all 16 waves be resident.
+template <int MODE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad(
     KParams p) {
-  affine_me_body<64, false>(p);
+  affine_me_body<64, false, MODE>(p);
 }
-// 128-class items: one 1024-thread workgroup per CU (81 KB of LDS), one lane
+// 128-class items: one 1024-thread workgroup per CU (~100 KB of LDS), one lane
 // per sub-block of a 128x128 CU.
-__global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_body<128, false>(p); }
+template <int MODE>
+__global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_body<128, false, MODE>(p); }
 // The same with PROF (vame_set_prof).
+template <int MODE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad_prof(
     KParams p) {
-  affine_me_body<64, true>(p);
+  affine_me_body<64, true, MODE>(p);
 }
-__global__ __launch_bounds__(1024) void affine_me_ctu_prof(KParams p) { affine_me_body<128, true>(p); }
+template <int MODE>
+__global__ __launch_bounds__(1024) void affine_me_ctu_prof(KParams p) { affine_me_body<128, true, MODE>(p); }
 
 }  // namespace vame
