@@ -149,6 +149,22 @@ long long vame_log_append(const char* prefix, int pred, int width, int height, i
                           const int64_t* cost, const vame_cpmvs* cpmvs, int nthreads);
 int vame_log_file_count(int pred);
 
+/* The same log, a whole POC per call (the CLI's path): a writer holds a
+ * persistent thread pool and the open files of one prefix.  One call appends
+ * the rows of every refIdx r < nrefs and PRED m in pred_mask (bit m), from the
+ * host arrays cost[r*4 + m] / cpmvs[r*4 + m] (entries of PREDs outside the
+ * mask may be NULL); the files receive exactly the bytes of the reference's
+ * per-(POC, refIdx, PRED) appends in main.cpp:942-958 order (refIdx outer,
+ * PRED inner).  Headers stay with vame_log_write_headers (POC 1, before the
+ * first call).  Returns the bytes written (< 0: error).
+ *   vame_log_writer_create : NULL on a bad prefix / unsupported resolution;
+ *                            nthreads <= 0: all host cores                   */
+typedef struct vame_log_writer vame_log_writer;
+vame_log_writer* vame_log_writer_create(const char* prefix, int width, int height, int nthreads);
+long long vame_log_writer_poc(vame_log_writer* w, int poc, int nrefs, int pred_mask,
+                              const int64_t* const* cost, const vame_cpmvs* const* cpmvs);
+int vame_log_writer_destroy(vame_log_writer* w);
+
 const char* vame_strerror(int code);
 const char* vame_last_hip_error(void);
 const char* vame_version(void);

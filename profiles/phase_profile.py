@@ -22,6 +22,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PHASES = ("stage", "predict", "cost", "gradient+reduce", "solve", "pass tail")
+# slots [kernel][phase + 6 * (3-CP pass)], 12 / 13: SIMD-slot use
 
 
 def main():
@@ -43,7 +44,7 @@ def main():
     d_o = [torch.from_numpy(orig[k].view(np.int16)).to(dev) for k in range(nf)]
     d_r = [torch.from_numpy(recon[k].view(np.int16)).to(dev) for k in range(nf)]
     eng = Engine(W, H, 0)
-    buf = np.zeros(16, np.uint64)
+    buf = np.zeros(32, np.uint64)
 
     def run():
         for poc in range(1, nf + 1):
@@ -57,12 +58,15 @@ def main():
     fn(buf.ctypes.data, 1)
     out = {}
     for k, name in enumerate(("affine_me_quad", "affine_me_ctu")):
-        v = buf[8 * k:8 * k + len(PHASES)].astype(np.float64)
+        v = buf[16 * k:16 * k + 12].astype(np.float64)
         tot = v.sum()
-        out[name] = {p: round(float(x / tot), 4) if tot else 0.0 for p, x in zip(PHASES, v)}
-        out[name]["wave_clock_total"] = float(tot)
-        slot, life = float(buf[8 * k + 6]), float(buf[8 * k + 7])
-        out[name]["simd_slot_use"] = round(life / slot, 4) if slot else 0.0
+        e = {}
+        for off, pas in ((0, "2cp"), (6, "3cp")):
+            e[pas] = {p: round(float(x / tot), 4) if tot else 0.0 for p, x in zip(PHASES, v[off:off + 6])}
+        e["wave_clock_total"] = float(tot)
+        slot, life = float(buf[16 * k + 12]), float(buf[16 * k + 13])
+        e["simd_slot_use"] = round(life / slot, 4) if slot else 0.0
+        out[name] = e
     print(json.dumps({"config": args.config, "steps": args.steps, "phases": out}, indent=1))
     eng.close()
 

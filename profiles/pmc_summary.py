@@ -33,7 +33,12 @@ PEAK_ISSUE = 0.5
 
 
 def short(name):
-    return name.split("(")[0].replace("vame::", "")
+    """Kernel name as the truncated trace prints it: "void vame::affine_me_quad<3>(...)"
+    -> "affine_me_quad" (one kernel instance per launch mode runs per config)."""
+    n = name.split("(")[0].replace("vame::", "")
+    if n.startswith("void "):
+        n = n[5:]
+    return n.split("<")[0]
 
 
 def counters(path):

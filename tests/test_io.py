@@ -236,3 +236,45 @@ def test_cli_no_device_or_bad_resolution(tmp_path):
         assert r.returncode == 0
     else:  # a GPU is present: then the inputs are missing
         assert r.returncode == 1 and "error while opening samples files" in r.stderr
+
+
+@pytest.mark.parametrize("size,nrefs,mask", [((416, 240), 2, 15), ((1920, 1080), 4, 15),
+                                             ((1280, 720), 3, 5)])
+def test_log_writer_poc_equals_appends(tmp_path, size, nrefs, mask):
+    """vame_log_writer_poc (a whole POC per call, persistent pool, files kept
+    open) writes the bytes of the reference-order per-(POC, refIdx, PRED)
+    appends, including the HALF names shared by several groups."""
+    W, H = size
+    rng = np.random.default_rng(W + nrefs)
+    n_ctus = logs.lib().vame_num_ctus(W, H)
+    preds = [m for m in range(4) if (mask >> m) & 1]
+    a, b = tmp_path / "writer", tmp_path / "appends"
+    a.mkdir()
+    b.mkdir()
+    with logs.LogWriter(str(a / "log"), W, H, nthreads=5) as wr:
+        for poc in (1, 2, 3):
+            res = {}
+            for r in range(min(nrefs, poc)):
+                for m in preds:
+                    n = n_ctus * (284 if m >> 1 else 201)
+                    cp = rng.integers(-70000, 70000, (n, 7)).astype(np.int32)
+                    res[(r, logs.PREDS[m])] = (rng.integers(0, 1 << 40, n), cp)
+            nb = logs.write_poc(str(a / "log"), W, H, poc, res, writer=wr)
+            nb2 = logs.write_poc(str(b / "log"), W, H, poc, res, nthreads=3)
+            assert nb == nb2 > 0
+    fa, fb = _files(a), _files(b)
+    assert fa == fb and len(fa) == sum(logs.lib().vame_log_file_count(m) for m in preds)
+    for f in fa:
+        assert (a / f).read_bytes() == (b / f).read_bytes(), f
+
+
+def test_log_writer_rejects_bad_arguments(tmp_path):
+    import ctypes
+    L = logs.lib()
+    assert not L.vame_log_writer_create(str(tmp_path / "x").encode(), 1000, 1000, 1)
+    w = L.vame_log_writer_create(str(tmp_path / "x").encode(), 416, 240, 1)
+    assert w
+    nul = (ctypes.c_void_p * 4)()
+    assert L.vame_log_writer_poc(w, 1, 1, 1, nul, nul) < 0  # PRED 0 in the mask without arrays
+    assert L.vame_log_writer_poc(w, 1, 5, 1, nul, nul) < 0  # more than 4 refs
+    assert L.vame_log_writer_destroy(w) == 0

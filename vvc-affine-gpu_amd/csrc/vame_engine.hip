@@ -543,13 +543,13 @@ const char* vame_strerror(int code) {
 const char* vame_last_hip_error(void) { return g_hip_err; }
 
 #if VAME_PHASE_TIMING
-// profiling-only builds: per-phase shader-clock sums [kernel][phase] (see vame_kernel.h)
-int vame_debug_phase_cycles(unsigned long long* out16, int reset) {
-  if (!out16) return VAME_E_INVALID;
+// profiling-only builds: per-phase shader-clock sums [kernel][pass phase] (see vame_kernel.h)
+int vame_debug_phase_cycles(unsigned long long* out32, int reset) {
+  if (!out32) return VAME_E_INVALID;
   VAME_HIP(hipDeviceSynchronize());
-  VAME_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 16));
+  VAME_HIP(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 32));
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[32] = {};
     VAME_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)));
   }
   return VAME_OK;

@@ -12,15 +12,28 @@
 //    per (POC, refIdx) in (group, CTU, cuIdx) order.  Rows are formatted with
 //    std::to_chars by a thread per CTU range and appended with one fwrite per
 //    group, so the bytes are identical to the reference's fprintf loop.
+//    vame_log_writer_* logs a whole POC per call on a persistent thread pool
+//    with the files kept open (the CLI's path): the rows of every (refIdx,
+//    PRED, group, CTU chunk) are formatted in parallel, then each file gets
+//    its rows with one writev, files in parallel.
 #include <fcntl.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <charconv>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -32,11 +45,97 @@ using namespace vame;
 
 namespace {
 
+// Host CPUs this process may use: its affinity mask, capped by a cgroup-v2
+// CPU quota (cpu.max) and by OMP_NUM_THREADS when set -- a GPU box can show
+// hundreds of CPUs while granting a process a 16-CPU share, and threads beyond
+// the share only get throttled.
+int host_threads() {
+  static const int n = [] {
+    int c = (int)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) c = CPU_COUNT(&set);
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long period = 0;
+      if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+        c = std::min<long>(c, std::max(1L, (atol(q) + period - 1) / period));
+      fclose(f);
+    }
+    if (const char* e = getenv("OMP_NUM_THREADS"))
+      if (atoi(e) > 0) c = std::min(c, atoi(e));
+    return std::max(1, c);
+  }();
+  return n;
+}
+
 int pick_threads(int requested, long work_items) {
-  int t = requested > 0 ? requested : (int)std::thread::hardware_concurrency();
+  int t = requested > 0 ? requested : host_threads();
   t = std::max(1, std::min(t, 64));
   return (int)std::max(1L, std::min<long>(t, work_items));
 }
+
+// Persistent workers for the log writer: run(n, f) calls f(i) for i < n on
+// the workers and the calling thread, and returns when all are done.
+class Pool {
+ public:
+  explicit Pool(int nthreads) {
+    for (int t = 1; t < nthreads; t++) th_.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void run(int n, const std::function<void(int)>& f) {
+    if (th_.empty() || n <= 1) {
+      for (int i = 0; i < n; i++) f(i);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = &f;
+      n_ = n;
+      next_.store(0);
+      active_ = (int)th_.size();
+      gen_++;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(mu_);
+    done_.wait(g, [&] { return active_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (int i; (i = next_.fetch_add(1)) < n_;) (*job_)(i);
+  }
+  void loop() {
+    unsigned long long seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+      std::lock_guard<std::mutex> g(mu_);
+      if (--active_ == 0) done_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* job_ = nullptr;
+  int n_ = 0, active_ = 0;
+  std::atomic<int> next_{0};
+  unsigned long long gen_ = 0;
+  bool stop_ = false;
+};
 
 template <class F>
 void parallel_for(int nthreads, int n, F&& f) {
@@ -140,17 +239,62 @@ inline void cu_pos(int align, int g, int cu, int ctu, int ctuCols, int& x, int& 
   x += (ctu % ctuCols) * 128;
 }
 
-inline char* put(char* p, long long v) { return std::to_chars(p, p + 24, v).ptr; }
+// Decimal text of an integer, as printf's %d / %ld: two digits per step from
+// a pair table, 32-bit arithmetic whenever the value fits (costs are < 2^31).
+constexpr char kPairs[201] =
+    "0001020304050607080910111213141516171819202122232425262728293031323334353637383940414243444546474849"
+    "5051525354555657585960616263646566676869707172737475767778798081828384858687888990919293949596979899";
+inline char* put_u32(char* p, uint32_t v) {
+  const int n = v < 10 ? 1 : v < 100 ? 2 : v < 1000 ? 3 : v < 10000 ? 4 : v < 100000 ? 5
+              : v < 1000000 ? 6 : v < 10000000 ? 7 : v < 100000000 ? 8 : v < 1000000000 ? 9 : 10;
+  char* q = p + n;
+  while (v >= 100) {
+    const uint32_t r = v % 100;
+    v /= 100;
+    q -= 2;
+    memcpy(q, kPairs + 2 * r, 2);
+  }
+  if (v >= 10) {
+    memcpy(q - 2, kPairs + 2 * v, 2);
+  } else {
+    q[-1] = (char)('0' + v);
+  }
+  return p + n;
+}
+inline char* put(char* p, long long v) {
+  if (v >= -2147483647ll && v <= 4294967295ll) {
+    if (v < 0) {
+      *p++ = '-';
+      return put_u32(p, (uint32_t)(-v));
+    }
+    return put_u32(p, (uint32_t)v);
+  }
+  return std::to_chars(p, p + 24, v).ptr;
+}
 
 // Rows of one (group, CTU range) in the reference's fprintf format
 // "%d,%d,%d,%d,%d,%d,%d,%ld,%d,%d,%d,%d,%d,%d\n" (main_aux_functions.h:491).
-void format_rows(std::string& buf, int align, int g, int ctu0, int ctu1, int ctuCols, int poc,
+// A reusable text buffer (grown without the zero fill of std::string::resize).
+struct Buf {
+  std::unique_ptr<char[]> d;
+  size_t cap = 0, len = 0;
+  char* reserve(size_t n) {
+    if (n > cap) {
+      d.reset(new char[n]);
+      cap = n;
+    }
+    return d.get();
+  }
+};
+
+void format_rows(Buf& buf, int align, int g, int ctu0, int ctu1, int ctuCols, int poc,
                  int ref, const int64_t* cost, const vame_cpmvs* cp) {
   const int ncu = align ? kHalfN[g] : (kFullStride[g + 1] - kFullStride[g]);
   const int stride = align ? kHalfStride[g] : kFullStride[g];
   const int T = align ? kHalfCusPerCtu : kFullCusPerCtu;
-  buf.resize((size_t)(ctu1 - ctu0) * ncu * 160);
-  char* p = &buf[0];
+  // a row is at most 4 x 11 + 3 x 5 + 20 + 6 x 11 + 14 separators < 160 bytes
+  char* const p0 = buf.reserve((size_t)(ctu1 - ctu0) * ncu * 160);
+  char* p = p0;
   char pre[32];
   char* pe = put(pre, poc);
   *pe++ = ',';
@@ -184,12 +328,164 @@ void format_rows(std::string& buf, int align, int g, int ctu0, int ctu1, int ctu
       *p++ = '\n';
     }
   }
-  buf.resize((size_t)(p - &buf[0]));
+  buf.len = (size_t)(p - p0);
+}
+
+// Process-wide pool of the per-call entry points (vame_log_append,
+// vame_read_frames keep their own threads): sized on first use.
+Pool& shared_pool(int nthreads) {
+  static std::mutex mu;
+  static std::unique_ptr<Pool> pool;
+  static int size = 0;
+  std::lock_guard<std::mutex> g(mu);
+  const int want = pick_threads(nthreads, 1 << 20);
+  if (!pool || size != want) {
+    pool.reset();
+    pool.reset(new Pool(want));
+    size = want;
+  }
+  return *pool;
 }
 
 }  // namespace
 
+// A POC-at-a-time decision-log writer (include/vame.h vame_log_writer_*).
+struct vame_log_writer {
+  std::string prefix;
+  int W = 0, H = 0, nCtus = 0, ctuCols = 0;
+  std::unique_ptr<Pool> pool;
+  // files: per pred, group -> file index (duplicate HALF names share a file)
+  std::vector<int> fileOf[4];
+  std::vector<std::string> paths;
+  std::vector<int> predOf;
+  std::vector<int> fds;
+  std::vector<Buf> bufs;  // per task, reused across POCs
+  ~vame_log_writer() {
+    for (int fd : fds)
+      if (fd >= 0) close(fd);
+  }
+};
+
+namespace {
+constexpr int kLogChunk = 64;  // CTUs per formatting task
+}
+
 extern "C" {
+
+vame_log_writer* vame_log_writer_create(const char* prefix, int width, int height, int nthreads) {
+  if (!prefix) return nullptr;
+  const int nCtus = num_ctus(width, height);
+  if (!nCtus) return nullptr;
+  auto* w = new vame_log_writer;
+  w->prefix = prefix;
+  w->W = width;
+  w->H = height;
+  w->nCtus = nCtus;
+  w->ctuCols = (width + kCtu - 1) / kCtu;
+  w->pool.reset(new Pool(pick_threads(nthreads, 1 << 20)));
+  std::map<std::string, int> idx;
+  for (int m = 0; m < 4; m++) {
+    const int ng = (m >> 1) ? kHalfGroups : kFullGroups;
+    for (int g = 0; g < ng; g++) {
+      const std::string p = log_path(prefix, m, g);
+      auto it = idx.find(p);
+      if (it == idx.end()) {
+        it = idx.emplace(p, (int)w->paths.size()).first;
+        w->paths.push_back(p);
+        w->predOf.push_back(m);
+      }
+      w->fileOf[m].push_back(it->second);
+    }
+  }
+  w->fds.assign(w->paths.size(), -1);
+  return w;
+}
+
+long long vame_log_writer_poc(vame_log_writer* w, int poc, int nrefs, int pred_mask,
+                              const int64_t* const* cost, const vame_cpmvs* const* cpmvs) {
+  if (!w || nrefs <= 0 || nrefs > 4 || !cost || !cpmvs || (pred_mask & ~15)) return VAME_E_INVALID;
+  for (int r = 0; r < nrefs; r++)
+    for (int m = 0; m < 4; m++)
+      if (((pred_mask >> m) & 1) && (!cost[r * 4 + m] || !cpmvs[r * 4 + m])) return VAME_E_INVALID;
+  const int nchunks = (w->nCtus + kLogChunk - 1) / kLogChunk;
+  // tasks in file order: refIdx, PRED, group, CTU chunk
+  struct Task {
+    int r, m, g, c;
+  };
+  std::vector<Task> tasks;
+  for (int r = 0; r < nrefs; r++)
+    for (int m = 0; m < 4; m++) {
+      if (!((pred_mask >> m) & 1)) continue;
+      const int ng = (m >> 1) ? kHalfGroups : kFullGroups;
+      for (int g = 0; g < ng; g++)
+        for (int c = 0; c < nchunks; c++) tasks.push_back({r, m, g, c});
+    }
+  if (w->bufs.size() < tasks.size()) w->bufs.resize(tasks.size());
+  w->pool->run((int)tasks.size(), [&](int i) {
+    const Task& t = tasks[i];
+    format_rows(w->bufs[i], t.m >> 1, t.g, t.c * kLogChunk, std::min(w->nCtus, (t.c + 1) * kLogChunk),
+                w->ctuCols, poc, t.r, cost[t.r * 4 + t.m], cpmvs[t.r * 4 + t.m]);
+  });
+  // per file, its tasks in order (a file belongs to one PRED; HALF names
+  // shared by several groups take them in group order, as the reference's
+  // per-group appends do)
+  std::vector<std::vector<int>> per(w->paths.size());
+  for (size_t i = 0; i < tasks.size(); i++) per[w->fileOf[tasks[i].m][tasks[i].g]].push_back((int)i);
+  std::vector<long long> wrote(w->paths.size(), 0);
+  std::atomic<int> bad{0};
+  w->pool->run((int)w->paths.size(), [&](int f) {
+    if (per[f].empty()) return;
+    int& fd = w->fds[f];
+    if (fd < 0) fd = open(w->paths[f].c_str(), O_WRONLY | O_APPEND | O_CREAT, 0644);
+    if (fd < 0) {
+      bad = 1;
+      return;
+    }
+    std::vector<iovec> iov;
+    for (int i : per[f])
+      if (w->bufs[i].len) iov.push_back({(void*)w->bufs[i].d.get(), w->bufs[i].len});
+    size_t k = 0;
+    while (k < iov.size()) {
+      const int cnt = (int)std::min<size_t>(iov.size() - k, 512);
+      size_t want = 0;
+      for (int j = 0; j < cnt; j++) want += iov[k + j].iov_len;
+      const ssize_t n = writev(fd, &iov[k], cnt);
+      if (n < 0 || (size_t)n != want) {  // short write: finish the batch by plain writes
+        size_t done = n < 0 ? 0 : (size_t)n;
+        for (int j = 0; j < cnt; j++) {
+          const size_t len = iov[k + j].iov_len;
+          if (done >= len) {
+            done -= len;
+            continue;
+          }
+          const char* q = (const char*)iov[k + j].iov_base + done;
+          size_t left = len - done;
+          done = 0;
+          while (left) {
+            const ssize_t m = write(fd, q, left);
+            if (m <= 0) {
+              bad = 1;
+              return;
+            }
+            q += m;
+            left -= (size_t)m;
+          }
+        }
+      }
+      wrote[f] += (long long)want;
+      k += (size_t)cnt;
+    }
+  });
+  if (bad) return VAME_E_INVALID;
+  long long total = 0;
+  for (long long b : wrote) total += b;
+  return total;
+}
+
+int vame_log_writer_destroy(vame_log_writer* w) {
+  delete w;
+  return VAME_OK;
+}
 
 int vame_read_frames(const char* path, int width, int height, int nframes, uint16_t* out,
                      int nthreads) {
@@ -295,8 +591,8 @@ long long vame_log_append(const char* prefix, int pred, int width, int height, i
   const int chunk = 64;
   const int nchunks = (nCtus + chunk - 1) / chunk;
   const int ntasks = ng * nchunks;
-  std::vector<std::string> out(ntasks);
-  parallel_for(pick_threads(nthreads, ntasks), ntasks, [&](int i, int) {
+  std::vector<Buf> out(ntasks);
+  shared_pool(nthreads).run(ntasks, [&](int i) {
     const int g = i / nchunks, c = i % nchunks;
     format_rows(out[i], align, g, c * chunk, std::min(nCtus, (c + 1) * chunk), ctuCols, poc, ref,
                 cost, cpmvs);
@@ -307,12 +603,12 @@ long long vame_log_append(const char* prefix, int pred, int width, int height, i
     FILE* f = fopen(p.c_str(), "a");
     if (!f) return VAME_E_INVALID;
     for (int c = 0; c < nchunks; c++) {
-      const std::string& s = out[g * nchunks + c];
-      if (fwrite(s.data(), 1, s.size(), f) != s.size()) {
+      const Buf& s = out[g * nchunks + c];
+      if (s.len && fwrite(s.d.get(), 1, s.len, f) != s.len) {
         fclose(f);
         return VAME_E_INVALID;
       }
-      total += (long long)s.size();
+      total += (long long)s.len;
     }
     fclose(f);
   }

@@ -110,7 +110,7 @@ struct KParams {
 #endif
 // VAME_DUP (timing-only builds, results stay correct): run a phase twice to
 // price it in throughput terms: bit 0 prediction, bit 1 gradient, bit 2
-// equation reduction, bit 4 the solve (on the system itself, before the real
+// equation reduction, bit 6 the tile staging round trip, bit 4 the solve (on the system itself, before the real
 // one rebuilds it: no extra LDS); with bit 5 set, only in the 3-CP pass.
 #ifndef VAME_DUP
 #define VAME_DUP 0
@@ -145,22 +145,23 @@ __device__ unsigned long long g_pred_count[2];
 #endif
 enum { kPhStage, kPhPredict, kPhCost, kPhGradient, kPhSolve, kPhTail, kNumPhases };
 #if VAME_PHASE_TIMING
-__device__ unsigned long long g_phase_cycles[2][8];  // [kernel: quad, ctu][phase]
-#define PH_DECL unsigned long long ph_acc[kNumPhases] = {}; unsigned long long ph_t = __builtin_amdgcn_s_memtime(); const unsigned long long ph_t0 = ph_t;
-#define PH_MARK(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_acc[i] += t_ - ph_t; ph_t = t_; }
-// plus SIMD-slot use: [6] = waves x block lifetime, [7] = sum of wave lifetimes
+// [kernel: quad, ctu][phase + 6 for the 3-CP pass; 12, 13: SIMD-slot use]
+__device__ unsigned long long g_phase_cycles[2][16];
+#define PH_DECL unsigned long long ph_acc[2 * kNumPhases] = {}; unsigned long long ph_t = __builtin_amdgcn_s_memtime(); const unsigned long long ph_t0 = ph_t;
+#define PH_MARK(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_acc[(i) + ph_off] += t_ - ph_t; ph_t = t_; }
+// plus SIMD-slot use: [12] = waves x block lifetime, [13] = sum of wave lifetimes
 __shared__ unsigned long long s_ph_blk[3];  // min start, max end, sum of lifetimes
 __shared__ int s_ph_done;
 #define PH_FLUSH { \
   if (lane == 0) { \
-    for (int i_ = 0; i_ < kNumPhases; i_++) atomicAdd(&g_phase_cycles[REGION == 128][i_], ph_acc[i_]); \
+    for (int i_ = 0; i_ < 2 * kNumPhases; i_++) atomicAdd(&g_phase_cycles[REGION == 128][i_], ph_acc[i_]); \
     const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
     atomicMax(&s_ph_blk[1], t1_); \
     atomicAdd(&s_ph_blk[2], t1_ - ph_t0); \
     const int nw_ = (int)(blockDim.x >> 6); \
     if (atomicAdd(&s_ph_done, 1) == nw_ - 1) { \
-      atomicAdd(&g_phase_cycles[REGION == 128][6], (unsigned long long)nw_ * (s_ph_blk[1] - s_ph_blk[0])); \
-      atomicAdd(&g_phase_cycles[REGION == 128][7], s_ph_blk[2]); \
+      atomicAdd(&g_phase_cycles[REGION == 128][12], (unsigned long long)nw_ * (s_ph_blk[1] - s_ph_blk[0])); \
+      atomicAdd(&g_phase_cycles[REGION == 128][13], s_ph_blk[2]); \
     } \
   } }
 #define PH_INIT { if (tid == 0) { s_ph_blk[0] = ~0ull; s_ph_blk[1] = 0; s_ph_blk[2] = 0; s_ph_done = 0; } }
@@ -1094,30 +1095,34 @@ struct Schedule {
   }
 };
 
+// One exchange of a halving step over lane bit B: a is the value the lanes
+// with bit B clear keep, b the one the others keep; returns this lane's kept
+// value summed with its partner's.
+template <int B>
+__device__ __forceinline__ long long pair_step(long long a, long long b) {
+  if constexpr (B >= 4) {
+    const unsigned al = (unsigned)(unsigned long long)a, ah = (unsigned)((unsigned long long)a >> 32);
+    const unsigned bl = (unsigned)(unsigned long long)b, bh = (unsigned)((unsigned long long)b >> 32);
+    // bit 5: lanes 0-31 end with a summed over (l, l^32), lanes 32-63 with b
+    const auto rl = B == 5 ? __builtin_amdgcn_permlane32_swap(al, bl, false, false)
+                           : __builtin_amdgcn_permlane16_swap(al, bl, false, false);
+    const auto rh = B == 5 ? __builtin_amdgcn_permlane32_swap(ah, bh, false, false)
+                           : __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
+    return (long long)(((unsigned long long)rh[0] << 32) | rl[0]) +
+           (long long)(((unsigned long long)rh[1] << 32) | rl[1]);
+  } else if constexpr (B == 3 || B == 2) {
+    return xchg_masked64<B>(a, b);
+  } else {
+    return sel_bit64<B>(a, b) + partner64<B>(sel_bit64<B>(b, a));
+  }
+}
 // Halving step over lane bit B on the first M values of x (the rest unused):
 // afterwards x[0 .. ceil(M/2)) holds this lane's kept half.
 template <int B, int M>
 __device__ __forceinline__ void halve64(long long* x) {
   constexpr int H = (M + 1) / 2;
 #pragma unroll
-  for (int j = 0; j < H; j++) {
-    const long long a = x[j], b = j + H < M ? x[j + H] : 0;
-    if constexpr (B >= 4) {
-      const unsigned al = (unsigned)(unsigned long long)a, ah = (unsigned)((unsigned long long)a >> 32);
-      const unsigned bl = (unsigned)(unsigned long long)b, bh = (unsigned)((unsigned long long)b >> 32);
-      // bit 5: lanes 0-31 end with a summed over (l, l^32), lanes 32-63 with b
-      const auto rl = B == 5 ? __builtin_amdgcn_permlane32_swap(al, bl, false, false)
-                             : __builtin_amdgcn_permlane16_swap(al, bl, false, false);
-      const auto rh = B == 5 ? __builtin_amdgcn_permlane32_swap(ah, bh, false, false)
-                             : __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
-      x[j] = (long long)(((unsigned long long)rh[0] << 32) | rl[0]) +
-             (long long)(((unsigned long long)rh[1] << 32) | rl[1]);
-    } else if constexpr (B == 3 || B == 2) {
-      x[j] = xchg_masked64<B>(a, b);
-    } else {
-      x[j] = sel_bit64<B>(a, b) + partner64<B>(sel_bit64<B>(b, a));
-    }
-  }
+  for (int j = 0; j < H; j++) x[j] = pair_step<B>(x[j], j + H < M ? x[j + H] : 0);
 }
 // Runs the halving steps while the count is > 1.  A remaining segment bit
 // after the count reached 1 becomes a plain sum (row_shr:2^B), valid in the
@@ -1174,9 +1179,22 @@ __device__ __forceinline__ void reduce_equations_64(const int (&S)[5], int u, in
                                                     long long* dst) {
   constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
   long long x[NV];
+  if constexpr (NCP == 3) {
+    // the first halving step is fused with the values' generation: moments
+    // j and j + 12 are formed and exchanged at once, so at most half of the
+    // 24 moments (48 VGPRs) are live -- this removed the 3-CP passes' spills
+    // (2-CP keeps the plain order: fusing its 14 values measured 1 % slower)
+    constexpr int H = ceil_half(NV);
+    constexpr int B0 = Schedule<LOGS>::bit(0);
 #pragma unroll
-  for (int i = 0; i < NV; i++) x[i] = eq_value<NCP>(i, S, u, v);
-  butterfly64<LOGS, 0, NV>(x);
+    for (int j = 0; j < H; j++)
+      x[j] = pair_step<B0>(eq_value<NCP>(j, S, u, v), j + H < NV ? eq_value<NCP>(j + H, S, u, v) : 0);
+    butterfly64<LOGS, 1, H>(x);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NV; i++) x[i] = eq_value<NCP>(i, S, u, v);
+    butterfly64<LOGS, 0, NV>(x);
+  }
   constexpr int CNT = final_count<LOGS, NV>();
   const int lidx = __lane_id() & ((1 << LOGS) - 1);
   int off, limit;
@@ -1234,11 +1252,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   __shared__ uint2 s_bot[C::NSB];  // row 3
   // the five gradient sums of every sub-block at its CU's best 2-CP iteration
   // (3-CP seed reuse, see the 3-CP init)
-#ifdef VAME_EXP_NOBESTS
-  __shared__ int s_bestS[5][1];
-#else
   __shared__ int s_bestS[5][C::NSB];
-#endif
   __shared__ __attribute__((aligned(16))) long long s_val[kMaxCu][kNumMom];
   __shared__ double s_mat[kMaxCu][42];  // per CU: N x (N + 1) system, N <= 6
   __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
@@ -1251,6 +1265,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
+  constexpr int ph_off = 0;  // phase-timing slots (3-CP pass: +kNumPhases)
+  (void)ph_off;
   PH_DECL
   PC_DECL
 
@@ -1287,6 +1303,20 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   constexpr int NCH = C::TILE * CPR;
   constexpr int PER = (NCH + C::THREADS - 1) / C::THREADS;
   uint4 tv[PER];
+  if constexpr ((VAME_DUP & 64) != 0) {  // timing-only: one extra staging round trip
+    if (!regionOut) {
+#pragma unroll
+      for (int j = 0; j < PER; j++) {
+        const int ch = tid + j * C::THREADS;
+        if (ch < NCH) {
+          const int ty = ch / CPR, cx = clampi((ch % CPR) * 8 + tx0, 0, W - 8);
+          tv[j] = *reinterpret_cast<const uint4*>(ref + (size_t)clampi(ty0 + ty, 0, H - 1) * W + cx);
+          *reinterpret_cast<uint4*>(&s_tile[(ch / CPR) * C::TP + (ch % CPR) * 8]) = tv[j];
+        }
+      }
+    }
+    __syncthreads();
+  }
   // stage the reference region (+margin) into LDS, clamp-to-edge padded, in
   // 16-byte chunks; a region wholly outside the frame (the bottom CTU row at
   // 1080p) has no in-frame CU: nothing is predicted, its tile is never read
@@ -1375,7 +1405,6 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     sy = (local >> (g.lw - 2)) << 2;
     active = (g.x + g.w <= W) && (g.y + g.h <= H);  // affine.cl:192-193
   }
-  const int sbTop = max(sbIdx - sbCols, 0), sbBot = min(sbIdx + sbCols, C::NSB - 1);
   const bool leader = myCu >= 0 && (lane & ((1 << logS) - 1)) == (1 << logS) - 1;
 
   // one copy of the pass per CP count and item class: ncp and coop are
@@ -1385,6 +1414,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     constexpr int ncp = decltype(ncpTag)::value;
     constexpr bool coop = decltype(coopTag)::value;
     constexpr bool keepS = decltype(keepTag)::value;  // 2-CP pass that feeds a 3-CP pass
+    constexpr int ph_off = ncp == 3 ? kNumPhases : 0;
+    (void)ph_off;
     constexpr int kDup = (VAME_DUP & 32) && ncp != 3 ? 0 : VAME_DUP;  // timing-only builds
     const int niter = (ncp == 3 ? 4 : 5) + p.extra;
 
@@ -1568,7 +1599,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           for (int k = 0; k < 5; k++) S[k] = s_bestS[k][sbIdx];
         } else if (live && !(VAME_ABLATE & 2)) {
           // the neighbours' edge rows, extended by the left / right lanes' copies
-          const uint2 tb = s_bot[sbTop], bt = s_top[sbBot];
+          // the sub-blocks above / below, computed here (kept live across the
+          // passes, the index was spilled)
+          const uint2 tb = s_bot[max(sbIdx - sbCols, 0)], bt = s_top[min(sbIdx + sbCols, C::NSB - 1)];
           X[0] = ext_row(tb, dpp32<0x138, 0xF>((int)tb.y), dpp32<0x130, 0xF>((int)tb.x));
           X[5] = ext_row(bt, dpp32<0x138, 0xF>((int)bt.y), dpp32<0x130, 0xF>((int)bt.x));
           Geo gg = g;

@@ -699,7 +699,13 @@ int main(int argc, char** argv) {
     if (!j.pocs.empty()) workers.emplace_back(gpu_worker, j);
   }
 
-  // ---- writer: POCs in order (main.cpp:954-958 -> main_aux_functions.h:387-525)
+  // ---- writer: POCs in order (main.cpp:954-958 -> main_aux_functions.h:387-525),
+  // a whole POC per vame_log_writer_poc call (persistent pool, files kept open)
+  vame_log_writer* logw = prefix.empty() ? nullptr : vame_log_writer_create(prefix.c_str(), W, H, nthreads);
+  if (!prefix.empty() && !logw) {
+    printf("  [!] ERROR: cannot create the log writer for %s_*\n", prefix.c_str());
+    return 1;
+  }
   float pred_ns[4] = {0, 0, 0, 0}, fused_ns = 0;
   long long log_bytes = 0;
   double log_s = 0;
@@ -717,11 +723,16 @@ int main(int argc, char** argv) {
       S.done.erase(p);
     }
     const float lambda = vame_lambda(qp, p);
+    const int predMask = (mode_mask & VAME_MODE_3CP) ? 15 : 5;
+    const int64_t* costs[16] = {};
+    const vame_cpmvs* cps[16] = {};
     for (int r = 0; r < s->nrefs; r++) {
       printf("POC   %d  RefIdx  %d  -> lambda %f\n", p, r, (double)lambda);
       for (int m = 0; m < 4; m++) {
-        if ((m & 1) && !(mode_mask & VAME_MODE_3CP)) continue;
+        if (!((predMask >> m) & 1)) continue;
         printf("Reporting results POC=%d refIdx=%d PredType=%d\n", p, r, m);
+        costs[r * 4 + m] = (const int64_t*)(s->host + L.off_cost[r][m]);
+        cps[r * 4 + m] = (const vame_cpmvs*)(s->host + L.off_cp[r][m]);
         if (prefix.empty()) continue;
         if (p == 1 && r == 0) {
           printf("Writing headers\n");
@@ -731,19 +742,19 @@ int main(int argc, char** argv) {
             break;
           }
         }
-        const double tl = now_s();
-        const long long nb =
-            vame_log_append(prefix.c_str(), m, W, H, p, r, (const int64_t*)(s->host + L.off_cost[r][m]),
-                            (const vame_cpmvs*)(s->host + L.off_cp[r][m]), nthreads);
-        log_s += now_s() - tl;
-        if (nb < 0) {
-          printf("  [!] ERROR: writing the log files %s_* failed\n", prefix.c_str());
-          ok = false;
-          break;
-        }
-        log_bytes += nb;
       }
       if (!ok) break;
+    }
+    if (ok && logw) {  // the POC's rows, every (refIdx, PRED) in the reference's order
+      const double tl = now_s();
+      const long long nb = vame_log_writer_poc(logw, p, s->nrefs, predMask, costs, cps);
+      log_s += now_s() - tl;
+      if (nb < 0) {
+        printf("  [!] ERROR: writing the log files %s_* failed\n", prefix.c_str());
+        ok = false;
+      } else {
+        log_bytes += nb;
+      }
     }
     for (int m = 0; m < 4; m++) pred_ns[m] += s->pred_ns[m];
     fused_ns += s->fused_ns;
@@ -759,6 +770,7 @@ int main(int argc, char** argv) {
     S.cv.notify_all();
   }
   for (auto& t : workers) t.join();
+  if (logw) vame_log_writer_destroy(logw);
   fflush(stdout);
   if (!S.error.empty() || !ok) {
     printf("  [!] ERROR: %s\n", S.error.empty() ? "log writer failed" : S.error.c_str());

@@ -15,6 +15,7 @@ EXPORTS = (
     "vame_ref_list", "vame_strerror", "vame_last_hip_error", "vame_version", "vame_set_timing",
     "vame_get_timing", "vame_read_frames", "vame_log_remove_old", "vame_log_write_headers",
     "vame_log_append", "vame_log_file_count", "vame_set_prof", "vame_affine_me_batch",
+    "vame_log_writer_create", "vame_log_writer_poc", "vame_log_writer_destroy",
 )
 
 
@@ -71,6 +72,11 @@ def lib():
         L.vame_log_append.argtypes = [C, I, I, I, I, I, P, P, I]
         L.vame_log_append.restype = ctypes.c_longlong
         L.vame_log_file_count.argtypes = [I]
+        L.vame_log_writer_create.argtypes = [C, I, I, I]
+        L.vame_log_writer_create.restype = P
+        L.vame_log_writer_poc.argtypes = [P, I, I, I, P, P]
+        L.vame_log_writer_poc.restype = ctypes.c_longlong
+        L.vame_log_writer_destroy.argtypes = [P]
         _lib = L
     return _lib
 

@@ -37,14 +37,7 @@ def write_headers(prefix: str, pred: int) -> None:
 def append(prefix: str, pred: int, width: int, height: int, poc: int, ref: int,
            cost: np.ndarray, cpmvs: np.ndarray, nthreads: int = 0) -> int:
     """Rows of one (POC, refIdx, pred); cost int64[n], cpmvs = [n, 7] int32 or CPMVS_DTYPE[n]."""
-    cost = np.ascontiguousarray(cost, np.int64)
-    cpmvs = np.ascontiguousarray(cpmvs)
-    if cpmvs.dtype != CPMVS_DTYPE:
-        cpmvs = np.ascontiguousarray(cpmvs, np.int32)
-        assert cpmvs.ndim == 2 and cpmvs.shape[1] == 7
-    n = lib().vame_num_ctus(width, height) * (284 if pred >> 1 else 201)
-    if cost.shape[0] != n or cpmvs.shape[0] != n:
-        raise ValueError(f"results must hold {n} entries")
+    cost, cpmvs = _arrays(pred, width, height, cost, cpmvs)
     nb = lib().vame_log_append(prefix.encode(), pred, width, height, poc, ref,
                                cost.ctypes.data_as(ctypes.c_void_p),
                                cpmvs.ctypes.data_as(ctypes.c_void_p), nthreads)
@@ -53,18 +46,86 @@ def append(prefix: str, pred: int, width: int, height: int, poc: int, ref: int,
     return nb
 
 
-def write_poc(prefix: str, width: int, height: int, poc: int, results, nthreads: int = 0) -> int:
+def _arrays(pred: int, width: int, height: int, cost: np.ndarray, cpmvs: np.ndarray):
+    cost = np.ascontiguousarray(cost, np.int64)
+    cpmvs = np.ascontiguousarray(cpmvs)
+    if cpmvs.dtype != CPMVS_DTYPE:
+        cpmvs = np.ascontiguousarray(cpmvs, np.int32)
+        assert cpmvs.ndim == 2 and cpmvs.shape[1] == 7
+    n = lib().vame_num_ctus(width, height) * (284 if pred >> 1 else 201)
+    if cost.shape[0] != n or cpmvs.shape[0] != n:
+        raise ValueError(f"results must hold {n} entries")
+    return cost, cpmvs
+
+
+class LogWriter:
+    """vame_log_writer: a whole POC per call on a persistent thread pool, files
+    kept open; the bytes of the reference's per-(POC, refIdx, PRED) appends."""
+
+    def __init__(self, prefix: str, width: int, height: int, nthreads: int = 0):
+        self.width, self.height = width, height
+        self._w = lib().vame_log_writer_create(prefix.encode(), width, height, nthreads)
+        if not self._w:
+            raise VameError(f"cannot create a log writer for {prefix} ({width}x{height})")
+
+    def poc(self, poc: int, results) -> int:
+        """results: {(ref, PRED name): (cost, cpmvs)}; refs 0..n-1, each with
+        the same PREDs."""
+        refs = sorted({r for r, _ in results})
+        if refs != list(range(len(refs))):
+            raise ValueError("refIdx must run 0..n-1")
+        mask = 0
+        for m, name in enumerate(PREDS):
+            if any((r, name) in results for r in refs):
+                mask |= 1 << m
+        keep = []
+        cost_p = (ctypes.c_void_p * (4 * len(refs)))()
+        cp_p = (ctypes.c_void_p * (4 * len(refs)))()
+        for r in refs:
+            for m, name in enumerate(PREDS):
+                if not (mask >> m) & 1:
+                    continue
+                if (r, name) not in results:
+                    raise ValueError(f"refIdx {r} lacks {name}")
+                c, p = _arrays(m, self.width, self.height, *results[(r, name)])
+                keep += [c, p]
+                cost_p[r * 4 + m] = c.ctypes.data
+                cp_p[r * 4 + m] = p.ctypes.data
+        nb = lib().vame_log_writer_poc(self._w, poc, len(refs), mask, cost_p, cp_p)
+        if nb < 0:
+            raise VameError("writing the log files failed")
+        return nb
+
+    def close(self) -> None:
+        if self._w:
+            lib().vame_log_writer_destroy(self._w)
+            self._w = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def write_poc(prefix: str, width: int, height: int, poc: int, results, nthreads: int = 0,
+              writer: LogWriter | None = None) -> int:
     """Log one POC like main.cpp:942-958: for each refIdx the four PREDs in
     order (headers first at POC 1 / refIdx 0).  results: {(ref, PRED name):
-    (cost, cpmvs)} as host arrays."""
-    nb = 0
+    (cost, cpmvs)} as host arrays.  With a LogWriter (same prefix) the POC
+    goes through it in one call."""
     refs = sorted({r for r, _ in results})
+    if poc == 1 and 0 in refs:
+        for m, name in enumerate(PREDS):
+            if (0, name) in results:
+                write_headers(prefix, m)
+    if writer is not None:
+        return writer.poc(poc, results)
+    nb = 0
     for r in refs:
         for m, name in enumerate(PREDS):
             if (r, name) not in results:
                 continue
-            if poc == 1 and r == 0:
-                write_headers(prefix, m)
             cost, cp = results[(r, name)]
             nb += append(prefix, m, width, height, poc, r, cost, cp, nthreads)
     return nb
