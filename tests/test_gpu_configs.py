@@ -14,6 +14,11 @@ sequence are checked against the per-POC entry point on the device.
                  and lambda): POCs 8 and 9 (long-term ref POC 0 / POC 8, the
                  QP+1 lambda of POC 8) per QP, and the whole 30-frame ring at
                  QP32
+  configs[4] C5  3840x2160 QP32, 240 frames sharded by POC over 8 GPUs: the
+                 last rank's block (POC 211-240, `shard.poc_shard(240, 8, 7)`)
+                 in one batched call -- the ring's long-term references at
+                 high POCs (POC 239: 238 232 224 216) and the QP+1 lambda of
+                 POC 240 -- three pairs vs the oracle, POCs vs per-POC calls
 """
 import numpy as np
 import pytest
@@ -162,3 +167,22 @@ def test_c4_2160p_30_frame_ring(engines):
     for poc, refidx in ((30, 3), (24, 1)):
         rp = ref_list(poc)[refidx]
         check_pair_vs_oracle(seq[poc], refidx, recon[rp], orig[poc], 3, f"C4 ring POC{poc} ref{refidx}(POC{rp})")
+
+
+def test_c5_2160p_last_shard_vs_oracle(engines):
+    """configs[4]: the block the 8th GPU codes of the 240-frame 4K sequence,
+    exactly as bench.py --config c5 --gpus 8 hands it to rank 7."""
+    from vame import synth
+    from vame.hostlogic import ref_list
+    from vame.shard import poc_shard
+    pocs = poc_shard(240, 8, 7)
+    assert pocs[0] > 200 and pocs[-1] == 240
+    refs = sorted({p for poc in pocs for p in ref_list(poc)})
+    orig, recon = synth.synth_pocs(3840, 2160, pocs, refs, 32)
+    eng = engines(3840, 2160)
+    seq = run_sequence(eng, orig, recon, 32, pocs, 3)
+    assert ref_list(239) == [238, 232, 224, 216]
+    check_batch_vs_per_poc(eng, {p: seq[p] for p in (pocs[0], 232, 239, 240)}, None, None, 3)
+    for poc, refidx in ((240, 0), (239, 3), (pocs[0], 2)):
+        rp = ref_list(poc)[refidx]
+        check_pair_vs_oracle(seq[poc], refidx, recon[rp], orig[poc], 3, f"C5 POC{poc} ref{refidx}(POC{rp})")
