@@ -27,6 +27,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import sys
 
 import numpy as np
 
@@ -146,11 +147,20 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file_
                          "libvame_synth.so")
 
 
+_warned = False
+
+
 def native():
-    """ctypes handle of lib/libvame_synth.so, or None when it is not built."""
-    global _native
+    """ctypes handle of lib/libvame_synth.so, or None when it is not built (or
+    VAME_SYNTH_NUMPY is set): the numpy specification is then used, with a
+    one-time warning -- it is ~50x slower (4K frames take seconds each)."""
+    global _native, _warned
     if _native is None:
         if not os.path.exists(_LIB_PATH) or os.environ.get("VAME_SYNTH_NUMPY"):
+            if not _warned and not os.environ.get("VAME_SYNTH_NUMPY"):
+                print(f"vame.synth: {_LIB_PATH} not built (make synth); using the numpy generator",
+                      file=sys.stderr)
+                _warned = True
             return None
         L = ctypes.CDLL(_LIB_PATH)
         I, D, P, U = ctypes.c_int, ctypes.c_double, ctypes.c_void_p, ctypes.c_uint64
