@@ -152,7 +152,10 @@ def main():
 
     ops = getattr(dist, "ReduceOp", None)
     tmax = all_reduce([elapsed], ops and ops.MAX)[0]
-    rows_total = all_reduce([float(rows_per_step * args.steps)], ops and ops.SUM)[0]
+    # whole-job totals: rows, in-frame rows, compulsory bytes (orig + ref frame + results per pair)
+    rows_total, inframe_total, compulsory_total = all_reduce(
+        [float(rows_per_step * args.steps), float(run.pairs * acc["rows_inframe"] * args.steps),
+         float(run.pairs * (2 * W * H * 2 + acc["rows"] * 36) * args.steps)], ops and ops.SUM)
     value = rows_total / tmax
 
     # the one exchange step, outside the timed steps: decision records to rank 0
@@ -210,6 +213,12 @@ def main():
                                           "frac": span_achieved / HBM_PEAK_GBS,
                                           "avg_launch_ms": span_ms / max(span_n, 1),
                                           "alg_bytes_per_launch": step_bytes / max(span_n, 1)}},
+        # SURVEY §8(d) companions: in-frame candidates (the rows the kernels
+        # predict; out-of-frame rows are logged with their initial cost) and the
+        # compulsory bytes (orig + ref frame + results per pair) over the step
+        "value_inframe": inframe_total / tmax,
+        "compulsory": {"bytes_per_step_all": compulsory_total / args.steps,
+                       "GBps": compulsory_total / tmax / 1e9 if tmax > 0 else 0.0},
         "gather": {"to": "rank 0", "backend": "none" if dist is None else dist.get_backend(),
                    "ms": gather_ms, "bytes_into_rank0": gather_bytes,
                    "check": check},
