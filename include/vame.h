@@ -34,7 +34,17 @@ typedef struct { int32_t x, y; } vame_mv;
 typedef struct { int32_t nCPs; vame_mv LT, RT, LB; } vame_cpmvs;
 
 enum { VAME_ALIGN_FULL = 0, VAME_ALIGN_HALF = 1 };
-enum { VAME_MODE_2CP = 1, VAME_MODE_3CP = 2 }; /* mode_mask bits; 3CP requires 2CP */
+/* mode_mask bits of the fused calls: 2CP (required), 3CP (seeded by 2CP), and
+ * an optional alignment selection -- FULL and/or HALF; neither bit = both, as
+ * the reference codes them (the vame CLI's --align) */
+enum { VAME_MODE_2CP = 1, VAME_MODE_3CP = 2, VAME_MODE_FULL = 4, VAME_MODE_HALF = 8 };
+/* The PREDs (bit m = FULL_2CP, FULL_3CP, HALF_2CP, HALF_3CP) a valid mode_mask
+ * codes: the vame_poc_result entries it writes, the log files it feeds. */
+static inline int vame_pred_mask(int mode_mask) {
+  const int ncp = (mode_mask & VAME_MODE_3CP) ? 3 : 1;                 /* 2CP [+ 3CP] per alignment */
+  const int sel = (mode_mask >> 2) & 3;
+  return ((sel == 0 || (sel & 1)) ? ncp : 0) | ((sel == 0 || (sel & 2)) ? ncp << 2 : 0);
+}
 
 enum {
   VAME_OK = 0,

@@ -112,6 +112,27 @@ def test_cli_per_launch_and_two_workers_identical(seq416):
     compare_dirs(out2, exp)
 
 
+def test_cli_align_selection(seq416):
+    """--align full / half (SURVEY §8f CLI extension): each run launches one
+    alignment's items only and writes exactly that alignment's files, byte
+    for byte the reference writer's; together they are the both-run."""
+    tmp, orig, recon, exp = seq416
+    seen = []
+    for align in ("full", "half"):
+        out, stdout = run_cli(tmp, 416, 240, 6, 32, ["--align", align], name=f"align_{align}")
+        files = sorted(os.listdir(out))
+        assert files and all(align.upper() in f for f in files), files
+        for f in files:
+            assert (out / f).read_bytes() == (exp / f).read_bytes(), f
+        t = {l.split(",")[0]: float(l.split(",")[1]) for l in stdout.splitlines()
+             if l.endswith(tuple("0123456789")) and "_EXEC," in l}
+        other = "HALF" if align == "full" else "FULL"
+        assert t[f"{other}_2CP_EXEC"] == 0 and t[f"{other}_3CP_EXEC"] == 0
+        assert t[f"{align.upper()}_2CP_EXEC"] > 0 and t[f"{align.upper()}_3CP_EXEC"] > 0
+        seen += files
+    assert sorted(seen) == sorted(os.listdir(exp))
+
+
 def test_cli_2cp_only_and_extra_iters(tmp_path):
     orig, recon = synth_sequence(416, 240, 3, qp=37, seed=0x1234)
     write_csv(str(tmp_path / "orig.csv"), orig)

@@ -113,6 +113,24 @@ def test_2cp_only_mode(engines):
         assert (hp[:, 0] == 2).all()
 
 
+@pytest.mark.parametrize("modes", [3 | 4, 3 | 8, 1 | 4, 1 | 8])
+def test_alignment_selection(engines, modes):
+    """mode_mask with VAME_MODE_FULL / VAME_MODE_HALF codes one alignment only
+    (only its items launch): exactly its PREDs come back, equal to the
+    reference's golden outputs, for every golden case's first pair."""
+    from vame.engine import MODES as ORDER, pred_mask
+    z = np.load(GOLDEN[0])
+    eng = engines(int(z["W"]), int(z["H"]))
+    out = eng.affine_me_poc(dev(z["cur"]), [dev(z["ref"])], float(z["lam"]), modes=modes,
+                            extra=int(z["extra"]))
+    want = {(0, ORDER[m]) for m in range(4) if (pred_mask(modes) >> m) & 1}
+    assert set(out) == want and len(want) == (2 if modes & 2 else 1)
+    for _, name in want:
+        hc, hp = host(out[(0, name)])
+        np.testing.assert_array_equal(hc, z[name + "_cost"], err_msg=name)
+        np.testing.assert_array_equal(cp6(hp), z[name + "_cpmv"], err_msg=name)
+
+
 REF_HARNESS = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle", "_ref", "ref_harness_hip")
 
 

@@ -219,6 +219,8 @@ def test_cli_help_and_parameter_errors(tmp_path):
         assert msg in r.stdout, msg
     r = _run(["--bogus", "1"], tmp_path)
     assert r.returncode == 1 and "unrecognised option" in r.stderr
+    r = _run(["-q", "32", "-f", "1", "-s", "416x240", "-o", "a", "-r", "b", "--align", "diag"], tmp_path)
+    assert r.returncode == 1 and "--align must be both, full or half" in r.stdout
     # boost-style forms: -q32, --QP=32, unique long prefix (--Frames), defaults reported
     r = _run(["-q32", "--Frames=3", "--Res", "416x240", "-o", "a", "-r", "b",
               "--ExtraGradientIter", "2"], tmp_path)
@@ -278,3 +280,20 @@ def test_log_writer_rejects_bad_arguments(tmp_path):
     assert L.vame_log_writer_poc(w, 1, 1, 1, nul, nul) < 0  # PRED 0 in the mask without arrays
     assert L.vame_log_writer_poc(w, 1, 5, 1, nul, nul) < 0  # more than 4 refs
     assert L.vame_log_writer_destroy(w) == 0
+
+
+def test_pred_mask_mirrors_the_abi(tmp_path):
+    """vame.engine.pred_mask == include/vame.h vame_pred_mask (compiled here)
+    for every valid mode mask: 2-CP [+ 3-CP] per alignment, both alignments
+    unless one is selected."""
+    from vame.engine import pred_mask
+    masks = (1, 3, 5, 7, 9, 11, 13, 15)
+    assert [pred_mask(m) for m in masks] == [5, 15, 1, 3, 4, 12, 5, 15]
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    src = tmp_path / "pm.c"
+    src.write_text('#include <stdio.h>\n#include "vame.h"\nint main(void) {\n'
+                   '  for (int m = 1; m < 16; m += 2) printf("%d ", vame_pred_mask(m));\n  return 0;\n}\n')
+    exe = tmp_path / "pm"
+    subprocess.run(["gcc", "-std=c11", "-I", inc, "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert [int(v) for v in out] == [pred_mask(m) for m in masks]

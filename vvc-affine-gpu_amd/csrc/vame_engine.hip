@@ -447,9 +447,11 @@ int vame_affine_me(vame_ctx* c, const uint16_t* ref, const uint16_t* cur, float 
 int vame_affine_me_batch(vame_ctx* c, const vame_poc_job* jobs, int njobs, int mode_mask,
                          int extra, void* stream) {
   if (!c || !jobs || njobs < 1) return VAME_E_INVALID;
-  if (!(mode_mask & VAME_MODE_2CP) || (mode_mask & ~3) || extra < 0 || extra > 64)
+  if (!(mode_mask & VAME_MODE_2CP) || (mode_mask & ~15) || extra < 0 || extra > 64)
     return VAME_E_INVALID;
   const bool run3 = (mode_mask & VAME_MODE_3CP) != 0;
+  const int preds = vame_pred_mask(mode_mask);  // alignment selection: only those items launch
+  const bool doFull = (preds & 1) != 0, doHalf = (preds & 4) != 0;
   for (int j = 0; j < njobs; j++) {
     const vame_poc_job& jb = jobs[j];
     if (!jb.cur || !jb.refs || !jb.out || jb.nrefs < 1) return VAME_E_INVALID;
@@ -457,7 +459,7 @@ int vame_affine_me_batch(vame_ctx* c, const vame_poc_job* jobs, int njobs, int m
     for (int r = 0; r < jb.nrefs; r++) {
       if (!jb.refs[r]) return VAME_E_INVALID;
       for (int m = 0; m < 4; m++) {
-        const bool need = (m & 1) ? run3 : true;
+        const bool need = ((preds >> m) & 1) != 0;
         if (need && (!jb.out->cost[r][m] || !jb.out->cpmvs[r][m])) return VAME_E_INVALID;
       }
     }
@@ -483,7 +485,7 @@ int vame_affine_me_batch(vame_ctx* c, const vame_poc_job* jobs, int njobs, int m
       }
       const bool last = j == njobs - 1 && r == jb.nrefs - 1;
       if (kp.nPairs == kMaxPairs || last) {
-        VAME_TRY(launch(c, kp, true, true, true, (hipStream_t)stream));
+        VAME_TRY(launch(c, kp, doFull, doHalf, doFull, (hipStream_t)stream));
         kp.nPairs = 0;
       }
     }

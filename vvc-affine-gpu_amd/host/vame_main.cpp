@@ -9,6 +9,7 @@
 //                             one host thread + context per device
 //               --devices L   explicit device list (e.g. 0,1,2,3)
 //               --modes all|2cp   all four PREDs (default) or the 2-CP ones
+//               --align both|full|half   both alignments (default) or one
 //               --per-launch  one launch per (refIdx, PRED) as the reference
 //                             does (per-PRED kernel times); default = fused
 //                             per-POC launch (vame_affine_me_poc)
@@ -395,7 +396,7 @@ void gpu_worker(Job J) {
       Slab* s = batch[0];
       for (int r = 0; r < s->nrefs; r++)
         for (int m = 0; m < 4; m++) {
-          if ((m & 1) && !(J.mode_mask & VAME_MODE_3CP)) continue;
+          if (!((vame_pred_mask(J.mode_mask) >> m) & 1)) continue;
           if (hipEventElapsedTime(&ms, evs[slot][r * 4 + m].first, evs[slot][r * 4 + m].second))
             return false;
           s->pred_ns[m] += ms * 1e6f;
@@ -451,7 +452,7 @@ void gpu_worker(Job J) {
       }
       for (int r = 0; r < nrefs; r++)
         for (int m = 0; m < 4; m++) {
-          if ((m & 1) && !(J.mode_mask & VAME_MODE_3CP)) continue;
+          if (!((vame_pred_mask(J.mode_mask) >> m) & 1)) continue;
           auto& e = evs[slot][r * 4 + m];
           GPU_CHECK(hipEventRecord(e.first, st), "hipEventRecord");
           VAME_CHECK(vame_affine_me(ctx, drecon[refs[r]], dorig[p], lambda, m >> 1, (m & 1) ? 3 : 2,
@@ -472,7 +473,7 @@ void gpu_worker(Job J) {
         for (int r = 0; r < nrefs; r++) {
           rp[j][r] = drecon[refs[r]];
           for (int m = 0; m < 4; m++) {
-            if ((m & 1) && !(J.mode_mask & VAME_MODE_3CP)) continue;
+            if (!((vame_pred_mask(J.mode_mask) >> m) & 1)) continue;
             out[j].cost[r][m] = (int64_t*)(base((int)j) + J.L->off_cost[r][m]);
             out[j].cpmvs[r][m] = (vame_cpmvs*)(base((int)j) + J.L->off_cp[r][m]);
           }
@@ -532,6 +533,7 @@ int main(int argc, char** argv) {
       {"CpmvLogFile", 'l', true, "", "Output files preffix with produced CPMVs"},
       {"gpus", 0, true, "1", "number of GPUs (POCs frame-sharded over DeviceIndex..+gpus-1)"},
       {"modes", 0, true, "all", "all = 2- and 3-CP affine, 2cp = 2-CP only"},
+      {"align", 0, true, "both", "both = aligned (FULL) and half-aligned (HALF) CUs, full / half = one of them"},
       {"threads", 0, true, "0", "host threads for CSV parsing and log formatting (0 = all)"},
       {"devices", 0, true, "", "explicit device list, e.g. 0,1,2 (overrides DeviceIndex/gpus; "
                                "a device may repeat: several contexts on one GPU)"},
@@ -553,7 +555,14 @@ int main(int argc, char** argv) {
     printf("  [!] ERROR: --modes must be all or 2cp\n");
     return 1;
   }
-  const int mode_mask = modes == "all" ? (VAME_MODE_2CP | VAME_MODE_3CP) : VAME_MODE_2CP;
+  const std::string align = c.str("align");
+  if (align != "both" && align != "full" && align != "half") {
+    printf("  [!] ERROR: --align must be both, full or half\n");
+    return 1;
+  }
+  const int mode_mask = (modes == "all" ? (VAME_MODE_2CP | VAME_MODE_3CP) : VAME_MODE_2CP) |
+                        (align == "full" ? VAME_MODE_FULL : align == "half" ? VAME_MODE_HALF : 0);
+  const int predMask = vame_pred_mask(mode_mask);  // the PREDs coded, launched and logged
   const int nthreads = c.num("threads");
 
   print_timestamp("START HOST");
@@ -723,7 +732,6 @@ int main(int argc, char** argv) {
       S.done.erase(p);
     }
     const float lambda = vame_lambda(qp, p);
-    const int predMask = (mode_mask & VAME_MODE_3CP) ? 15 : 5;
     const int64_t* costs[16] = {};
     const vame_cpmvs* cps[16] = {};
     for (int r = 0; r < s->nrefs; r++) {
@@ -785,7 +793,7 @@ int main(int argc, char** argv) {
   if (!per_launch) {  // fused launches: apportion by each PRED's algorithmic work
     double wgt[4], sum = 0;
     for (int m = 0; m < 4; m++) {
-      wgt[m] = ((m & 1) && !(mode_mask & VAME_MODE_3CP)) ? 0 : pred_work(W, H, m >> 1, (m & 1) ? 3 : 2, extra);
+      wgt[m] = !((predMask >> m) & 1) ? 0 : pred_work(W, H, m >> 1, (m & 1) ? 3 : 2, extra);
       sum += wgt[m];
     }
     for (int m = 0; m < 4; m++) pred_ns[m] = (float)((double)fused_ns * wgt[m] / sum);

@@ -20,6 +20,15 @@ from ._lib import PocJob, PocResult, check, lib
 
 CPMV_FIELDS = ("nCPs", "LTx", "LTy", "RTx", "RTy", "LBx", "LBy")
 MODES = ("FULL_2CP", "FULL_3CP", "HALF_2CP", "HALF_3CP")
+# mode_mask bits (include/vame.h): 2-CP, 3-CP, and the alignment selection
+MODE_2CP, MODE_3CP, MODE_FULL, MODE_HALF = 1, 2, 4, 8
+
+
+def pred_mask(modes: int) -> int:
+    """vame_pred_mask: the PREDs (bit m of MODES) a mode mask codes."""
+    ncp = 3 if modes & MODE_3CP else 1
+    sel = (modes >> 2) & 3
+    return (ncp if sel in (0, 1, 3) else 0) | ((ncp << 2) if sel in (0, 2, 3) else 0)
 
 
 def _ptr(t: torch.Tensor | None):
@@ -110,16 +119,16 @@ class Engine:
 
     def alloc_poc(self, nrefs: int, modes: int = 3):
         res = {}
+        preds = pred_mask(modes)
         for r in range(nrefs):
             for m, name in enumerate(MODES):
-                if (m & 1) and not (modes & 2):
-                    continue
-                res[(r, name)] = self.alloc_result(m >> 1)
+                if (preds >> m) & 1:
+                    res[(r, name)] = self.alloc_result(m >> 1)
         return res
 
     def _check_poc_out(self, out, nrefs: int, modes: int):
-        need = {(r, name) for r in range(nrefs) for m, name in enumerate(MODES)
-                if not ((m & 1) and not (modes & 2))}
+        preds = pred_mask(modes)
+        need = {(r, name) for r in range(nrefs) for m, name in enumerate(MODES) if (preds >> m) & 1}
         missing = need - set(out)
         if missing:
             raise ValueError(f"result buffers missing for {sorted(missing)}")
@@ -153,7 +162,8 @@ class Engine:
         return [job[3] for job in jobs]
 
     def affine_me_poc(self, cur, refs, lam: float, modes: int = 3, extra: int = 0, out=None):
-        """modes: 1 = 2-CP only, 3 = 2-CP then 3-CP.  Returns {(refIdx, MODE): (cost, cpmv)}."""
+        """modes: 1 = 2-CP only, 3 = 2-CP then 3-CP, plus MODE_FULL / MODE_HALF to
+        code one alignment only.  Returns {(refIdx, MODE): (cost, cpmv)}."""
         cur = self._frame(cur)
         refs = [self._frame(r) for r in refs]
         out = out if out is not None else self.alloc_poc(len(refs), modes)
