@@ -40,11 +40,7 @@ enum { VAME_ALIGN_FULL = 0, VAME_ALIGN_HALF = 1 };
 enum { VAME_MODE_2CP = 1, VAME_MODE_3CP = 2, VAME_MODE_FULL = 4, VAME_MODE_HALF = 8 };
 /* The PREDs (bit m = FULL_2CP, FULL_3CP, HALF_2CP, HALF_3CP) a valid mode_mask
  * codes: the vame_poc_result entries it writes, the log files it feeds. */
-static inline int vame_pred_mask(int mode_mask) {
-  const int ncp = (mode_mask & VAME_MODE_3CP) ? 3 : 1;                 /* 2CP [+ 3CP] per alignment */
-  const int sel = (mode_mask >> 2) & 3;
-  return ((sel == 0 || (sel & 1)) ? ncp : 0) | ((sel == 0 || (sel & 2)) ? ncp << 2 : 0);
-}
+int vame_pred_mask(int mode_mask);
 
 enum {
   VAME_OK = 0,

@@ -444,6 +444,12 @@ int vame_affine_me(vame_ctx* c, const uint16_t* ref, const uint16_t* cur, float 
   return launch(c, kp, align == 0, align == 1, align == 0, (hipStream_t)stream);
 }
 
+int vame_pred_mask(int mode_mask) {
+  const int ncp = (mode_mask & VAME_MODE_3CP) ? 3 : 1;  // 2CP [+ 3CP] per alignment
+  const int sel = (mode_mask >> 2) & 3;                  // neither selection bit: both
+  return ((sel == 0 || (sel & 1)) ? ncp : 0) | ((sel == 0 || (sel & 2)) ? ncp << 2 : 0);
+}
+
 int vame_affine_me_batch(vame_ctx* c, const vame_poc_job* jobs, int njobs, int mode_mask,
                          int extra, void* stream) {
   if (!c || !jobs || njobs < 1) return VAME_E_INVALID;

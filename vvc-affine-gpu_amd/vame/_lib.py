@@ -15,7 +15,7 @@ EXPORTS = (
     "vame_ref_list", "vame_strerror", "vame_last_hip_error", "vame_version", "vame_set_timing",
     "vame_get_timing", "vame_read_frames", "vame_log_remove_old", "vame_log_write_headers",
     "vame_log_append", "vame_log_file_count", "vame_set_prof", "vame_affine_me_batch",
-    "vame_log_writer_create", "vame_log_writer_poc", "vame_log_writer_destroy",
+    "vame_log_writer_create", "vame_log_writer_poc", "vame_log_writer_destroy", "vame_pred_mask",
 )
 
 
