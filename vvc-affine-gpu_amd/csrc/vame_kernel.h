@@ -1011,9 +1011,9 @@ __device__ __forceinline__ int seg_sum_c(int v) {
 // the second half to the partner lane (lane ^ 2^b), which keeps the second
 // half -- so each step halves the values a lane holds and doubles the lanes
 // they are summed over.  Steps run cheapest first, while the counts are
-// largest: bit 5 (v_permlane32_swap), bit 4 (v_permlane16_swap), bits 3 and 2
-// (two bank-masked DPP add pairs), bits 1 and 0 (selects and a DPP quad_perm
-// add).  After the last step every value is held, fully summed, by exactly one
+// largest: bits 3 and 2 (two bank-masked DPP add pairs), bit 5
+// (v_permlane32_swap), bit 4 (v_permlane16_swap), bits 1 and 0 (selects and a
+// DPP quad_perm add; in practice plain row sums, the counts being 1 by then).  After the last step every value is held, fully summed, by exactly one
 // lane of the segment, which stores it (autonomous items: int64 slots) or adds
 // it (cooperative items: int64 LDS atomics across waves).  Integer sums: the
 // order is free.
@@ -1079,12 +1079,17 @@ __device__ __forceinline__ long long xchg_masked64(long long a, long long b) {
 
 constexpr int ceil_half(int m) { return (m + 1) / 2; }
 
-// Step order for a segment of 2^LOGS lanes: bits 5 4 3 2 1 0, restricted to
-// bits < LOGS.
+// Step order for a segment of 2^LOGS lanes: bits 3 2 5 4 1 0, restricted to
+// bits < LOGS -- cheapest per pair-step first, while the counts are largest:
+// a bank-masked DPP step (bits 3, 2) is ~11 SIMD cycles per int64 pair, a
+// permlane swap step (bits 5, 4) ~14 (v_permlane32_swap issues at ~5.3
+// cycles, profiles/r01_valu_rate.txt), a quad step (bits 1, 0) ~16.  The
+// counts reach 1 before bits 1 / 0, which then become plain DPP row sums.
+// (Round 1 ran 5 4 3 2 1 0; this order: c2 -0.6 %, c3 -0.3 %.)
 template <int LOGS>
 struct Schedule {
   static constexpr int bit(int i) {
-    constexpr int all[6] = {5, 4, 3, 2, 1, 0};
+    constexpr int all[6] = {3, 2, 5, 4, 1, 0};
     int n = 0;
     for (int k = 0; k < 6; k++)
       if (all[k] < LOGS) {
@@ -1179,21 +1184,18 @@ __device__ __forceinline__ void reduce_equations_64(const int (&S)[5], int u, in
                                                     long long* dst) {
   constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
   long long x[NV];
-  if constexpr (NCP == 3) {
-    // the first halving step is fused with the values' generation: moments
-    // j and j + 12 are formed and exchanged at once, so at most half of the
-    // 24 moments (48 VGPRs) are live -- this removed the 3-CP passes' spills
-    // (2-CP keeps the plain order: fusing its 14 values measured 1 % slower)
+  {
+    // the first halving step is fused with the values' generation: values
+    // j and j + NV/2 are formed and exchanged at once, so at most half of them
+    // are live (for the 24 3-CP moments this removed the 3-CP passes' spills;
+    // for the 14 2-CP values it is neutral to -0.2 % since the bank-masked
+    // steps run first)
     constexpr int H = ceil_half(NV);
     constexpr int B0 = Schedule<LOGS>::bit(0);
 #pragma unroll
     for (int j = 0; j < H; j++)
       x[j] = pair_step<B0>(eq_value<NCP>(j, S, u, v), j + H < NV ? eq_value<NCP>(j + H, S, u, v) : 0);
     butterfly64<LOGS, 1, H>(x);
-  } else {
-#pragma unroll
-    for (int i = 0; i < NV; i++) x[i] = eq_value<NCP>(i, S, u, v);
-    butterfly64<LOGS, 0, NV>(x);
   }
   constexpr int CNT = final_count<LOGS, NV>();
   const int lidx = __lane_id() & ((1 << LOGS) - 1);
