@@ -1050,26 +1050,29 @@ __device__ __forceinline__ long long partner64(long long v) {
 // with the bit clear get a + partner(a), the others b + partner(b) (a lane's
 // DPP source reads happen before any lane writes).  Each 64-bit add is
 // v_add_co / v_addc_co with DPP; the carry in VCC stays within the lanes one
-// masked pair enables.  Hazard waits are explicit: the backend does not look
-// inside inline asm.
+// masked pair enables.  Hazard waits are explicit (the backend does not look
+// inside inline asm): one s_nop 1 ahead of the block covers a DPP read of a
+// register the preceding VALU instruction wrote; inside the block every DPP
+// source (a's and b's halves) was written before it, so no further waits
+// (round 1 waited before each of the four: c3 -1 % without them).
 template <int B>
 __device__ __forceinline__ long long xchg_masked64(long long a, long long b) {
   unsigned al = (unsigned)(unsigned long long)a, ah = (unsigned)((unsigned long long)a >> 32);
   const unsigned bl = (unsigned)(unsigned long long)b, bh = (unsigned)((unsigned long long)b >> 32);
   if constexpr (B == 3) {
     asm("s_nop 1\n\tv_add_co_u32_dpp %0, vcc, %0, %0 row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
-        "s_nop 1\n\tv_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
-        "s_nop 1\n\tv_add_co_u32_dpp %0, vcc, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
-        "s_nop 1\n\tv_addc_co_u32_dpp %1, vcc, %3, %3, vcc row_ror:8 row_mask:0xf bank_mask:0xc"
+        "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
+        "v_add_co_u32_dpp %0, vcc, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
+        "v_addc_co_u32_dpp %1, vcc, %3, %3, vcc row_ror:8 row_mask:0xf bank_mask:0xc"
         : "+v"(al), "+v"(ah)
         : "v"(bl), "v"(bh)
         : "vcc");
   } else {
     static_assert(B == 2, "bank bits only");
     asm("s_nop 1\n\tv_add_co_u32_dpp %0, vcc, %0, %0 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
-        "s_nop 1\n\tv_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
-        "s_nop 1\n\tv_add_co_u32_dpp %0, vcc, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
-        "s_nop 1\n\tv_addc_co_u32_dpp %1, vcc, %3, %3, vcc row_shr:4 row_mask:0xf bank_mask:0xa"
+        "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+        "v_add_co_u32_dpp %0, vcc, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+        "v_addc_co_u32_dpp %1, vcc, %3, %3, vcc row_shr:4 row_mask:0xf bank_mask:0xa"
         : "+v"(al), "+v"(ah)
         : "v"(bl), "v"(bh)
         : "vcc");
