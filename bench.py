@@ -12,7 +12,7 @@ vame_affine_me_batch call.  Default = BASELINE.json configs[1]: 1920x1080
 QP32, 2 frames, 2-CPMV affine only (3 pairs, 196,425 candidate CUs per step).
 
 Multi-GPU (torchrun, one rank per GPU): every rank codes the
-contiguous POC block shard.poc_shard(n, world, rank) of ONE sequence (the same
+contiguous (POC, refIdx) pair block shard.pair_shard(n, world, rank) of ONE sequence (the same
 synthetic seed on every rank), with no collective on the data path.
   c2 / c3 / c4 scale weakly: the sequence has frames x N POCs, so every rank
                codes about `frames` POCs (c2 at N = 1 is exactly configs[1]);
@@ -195,7 +195,7 @@ def main():
                    "pairs_per_step_rank0": run.pairs, "rows_per_step_rank0": rows_per_step,
                    "rows_per_step_all": rows_total / args.steps,
                    "modes": "2cp+3cp" if modes & 2 else "2cp",
-                   "parallelism": f"frame-shard x{world} (poc_shard of one sequence)"},
+                   "parallelism": f"frame-shard x{world} (pair_shard of one sequence)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": prof.get("traffic"),
                      "kernel": "affine_me_quad",
@@ -306,12 +306,13 @@ def cpu_baseline(run, acc, ncps, W, H, modes, min_seconds=10.0):
     threads, cpus = host_cpus()
     orig, recon = synth.synth_pocs(W, H, run.pocs, sorted({p for q in run.pocs for p in ref_list(q)}),
                                    run.qp, run.seed)
-    pairs = [(poc, r, rp, job[2], job[3]) for poc, job in zip(run.pocs, run.jobs)
-             for r, rp in enumerate(ref_list(poc))]
+    # (POC, refIdx, ref POC, lambda, the job's results, key position in the job)
+    pairs = [(poc, r, ref_list(poc)[r], job[2], job[3], j) for (poc, refs), job in zip(run.blocks, run.jobs)
+             for j, r in enumerate(refs)]
     names = (("FULL_2CP", (0, 2)), ("FULL_3CP", (0, 3)), ("HALF_2CP", (1, 2)), ("HALF_3CP", (1, 3)))
     rows, dt, ok, checked, k = 0, 0.0, True, set(), 0
     while dt < min_seconds or k == 0:
-        poc, r, rp, lam, out = pairs[k % len(pairs)]
+        poc, r, rp, lam, out, j = pairs[k % len(pairs)]
         t0 = time.perf_counter()
         res = O.affine_me_pair(recon[rp], orig[poc], lam, 0, modes=ncps, nthreads=threads)
         dt += time.perf_counter() - t0
@@ -321,7 +322,7 @@ def cpu_baseline(run, acc, ncps, W, H, modes, min_seconds=10.0):
             for name, key in names:
                 if key not in res:
                     continue
-                c, p = out[(r, name)]
+                c, p = out[(j, name)]
                 oc, op = res[key]
                 gp = p.cpu().numpy()[:, 1:]
                 opp = np.stack([op[f] for f in ("LTx", "LTy", "RTx", "RTy", "LBx", "LBy")], 1)

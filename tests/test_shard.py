@@ -79,6 +79,34 @@ def test_poc_shard_covers_and_balances():
                 assert max(loads) - min(loads) <= 4
 
 
+def test_pair_shard_covers_and_balances():
+    for n in (1, 2, 4, 5, 16, 30, 240):
+        for world in (1, 2, 4, 8):
+            blocks = [shard.pair_shard(n, world, r) for r in range(world)]
+            flat = [(p, r) for b in blocks for p, refs in b for r in refs]
+            assert flat == [(p, r) for p in range(1, n + 1) for r in range(min(4, p))]
+            loads = [sum(len(refs) for _, refs in b) for b in blocks]
+            assert max(loads) - min(loads) <= 1
+            for b in blocks:  # one entry per POC, refIdx contiguous
+                assert len({p for p, _ in b}) == len(b)
+                assert all(refs == list(range(refs[0], refs[0] + len(refs))) for _, refs in b)
+    # the c2 weak-scaling sequences (2N POCs): 2 ranks of POC 1-4 split 5 / 5
+    # pairs (a whole-POC cut can do no better than 6 / 4)
+    assert [sum(len(x) for _, x in shard.pair_shard(4, 2, r)) for r in range(2)] == [5, 5]
+    assert shard.pair_shard(4, 2, 1) == [(3, [2]), (4, [0, 1, 2, 3])]
+
+
+def test_merge_blocks_rejoins_split_pocs():
+    blocks = [shard.pair_shard(4, 2, r) for r in range(2)]
+    res = [[{(j, "FULL_2CP"): (poc, refs[j]) for j in range(len(refs))} for poc, refs in b]
+           for b in blocks]
+    merged = shard.merge_blocks(blocks, res)
+    assert sorted(merged) == [1, 2, 3, 4]
+    for poc, d in merged.items():
+        assert sorted(d) == [(r, "FULL_2CP") for r in range(min(4, poc))]
+        assert all(v == (poc, r) for (r, _), v in d.items())
+
+
 def test_pack_unpack_roundtrip():
     g = torch.Generator().manual_seed(1)
     def rec(n, ncp):  # ABI records as the kernels write them: nCPs, 2-CP LB = 0, cost < 2^31
@@ -135,11 +163,10 @@ def gpu_worker(rank, world, port, outdir):
     if rank == 0:
         check = run.verify(slabs)
         assert check["byte_identical"], check
-        allres = []
-        for r in range(world):
-            allres += shard.unpack(slabs[r], layout(shard.poc_shard(NF, world, r)))
-        torch.save([{f"{k[0]}:{k[1]}": (c.clone(), p.clone()) for k, (c, p) in res.items()}
-                    for res in allres],
+        merged = shard.merge_blocks([shard.pair_shard(NF, world, r) for r in range(world)],
+                                    [shard.unpack(slabs[r], run.layout(r)) for r in range(world)])
+        torch.save([{f"{k[0]}:{k[1]}": (c.clone().cpu(), p.clone().cpu())
+                     for k, (c, p) in merged[poc].items()} for poc in sorted(merged)],
                    os.path.join(outdir, "gathered_gpu.pt"))
     dist.barrier()
     eng.close()
@@ -202,7 +229,7 @@ SEQ_W, SEQ_H, SEQ_N = 416, 240, 5  # 4x2 CTUs (last row 112 px high), POC 1..5 -
 
 def bench_path_worker(rank, world, port, outdir):
     """bench.py's multi-GPU path with the compute swapped for the oracle:
-    ShardRun over poc_shard of one sequence, step, gather to rank 0, rank 0's
+    ShardRun over pair_shard of one sequence, step, gather to rank 0, rank 0's
     recompute-and-compare check."""
     from vame.seqrun import ShardRun
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -225,7 +252,7 @@ def bench_path_worker(rank, world, port, outdir):
 @pytest.mark.timeout(600)
 def test_bench_shard_path_two_ranks_equals_single_process(tmp_path):
     """The exact sequence-shard path bench.py --gpus N runs (vame/seqrun.py:
-    one sequence, poc_shard per rank, one gather into rank 0, rank 0's sampled
+    one sequence, pair_shard per rank (POC 4 split between the ranks), one gather into rank 0, rank 0's sampled
     recompute check), on 2 gloo ranks: the gathered records equal a 1-rank run
     of the whole sequence word for word, and rank 0's own check passes."""
     from vame.seqrun import ShardRun
@@ -239,8 +266,7 @@ def test_bench_shard_path_two_ranks_equals_single_process(tmp_path):
     whole = single.slab()
     ofs = 0
     for r in range(2):
-        pocs = shard.poc_shard(SEQ_N, 2, r)
-        n = shard.slab_words([(len(ref_list(p)), 3, (single.n_cus)) for p in pocs])
+        n = shard.slab_words(shard.block_layout(shard.pair_shard(SEQ_N, 2, r), 3, single.n_cus))
         assert torch.equal(got["slabs"][r][:n], whole[ofs:ofs + n]), r
         assert not got["slabs"][r][n:].any()  # zero padding to the largest shard
         ofs += n

@@ -3,9 +3,9 @@
 The reference codes a sequence POC by POC (main.cpp:578-585: POC 1..N, refs
 from the 4-slot ring at :591-707, lambda from computeDeltaQp at :585).  No
 result feeds another POC, so the POCs shard over ranks: every rank takes the
-contiguous block `shard.poc_shard(n, world, rank)` of the SAME sequence (same
-synthetic seed), synthesizes only the frames that block reads (its originals
-and the recon frames of its refs), and codes it with no collective on the data
+contiguous pair block `shard.pair_shard(n, world, rank)` of the SAME sequence
+(same synthetic seed), synthesizes only the frames that block reads (its
+originals and the recon frames of its refs), and codes it with no collective on the data
 path.  The one exchange is the decision-record gather into rank 0
 (`shard.gather_to_root`, RCCL over xGMI), after which rank 0 can recompute a
 sample of every other rank's POCs and check the gathered records byte for byte.
@@ -26,12 +26,8 @@ from . import shard, synth
 from .hostlogic import lambda_for_poc, ref_list
 
 
-def sequence_layout(pocs, modes: int, n_cus_per_align: tuple[int, int]):
-    return [(len(ref_list(p)), modes, n_cus_per_align) for p in pocs]
-
-
 class ShardRun:
-    """POC block `poc_shard(n_frames, world, rank)` of the sequence
+    """Pair block `pair_shard(n_frames, world, rank)` of the sequence
     (W, H, qp, n_frames, seed), coded with `engine` on `device`."""
 
     def __init__(self, engine, W: int, H: int, qp: int, n_frames: int, modes: int, world: int,
@@ -39,26 +35,32 @@ class ShardRun:
         self.eng, self.W, self.H, self.qp, self.n = engine, W, H, qp, n_frames
         self.modes, self.world, self.rank, self.device, self.seed = modes, world, rank, device, seed
         self.n_cus = (engine.n_cus(0), engine.n_cus(1))
-        self.pocs = shard.poc_shard(n_frames, world, rank)
+        self.blocks = shard.pair_shard(n_frames, world, rank)
+        self.pocs = [p for p, _ in self.blocks]
         t0 = time.perf_counter()
-        self.jobs = self._jobs(self.pocs)
+        self.jobs = self._jobs(self.blocks)
         self.synth_s = time.perf_counter() - t0
         self.pairs = sum(len(j[1]) for j in self.jobs)
         # every rank's slab is padded to the largest shard's words (equal-size gather)
-        self.words = max(shard.slab_words(sequence_layout(shard.poc_shard(n_frames, world, r), modes,
-                                                          self.n_cus))
-                         for r in range(world))
+        self.words = max(shard.slab_words(self.layout(r)) for r in range(world))
 
-    def _jobs(self, pocs):
-        refs = sorted({p for poc in pocs for p in ref_list(poc)})
-        orig, recon = synth.synth_pocs(self.W, self.H, pocs, refs, self.qp, self.seed)
+    def layout(self, rank: int):
+        """`shard.unpack` layout of `rank`'s slab."""
+        return shard.block_layout(shard.pair_shard(self.n, self.world, rank), self.modes, self.n_cus)
+
+    def _jobs(self, blocks):
+        """One engine job per (POC, [refIdx...]) entry; the job's results are
+        keyed by the position in that refIdx list."""
+        rps = {poc: [ref_list(poc)[i] for i in refs] for poc, refs in blocks}
+        pocs = [p for p, _ in blocks]
+        orig, recon = synth.synth_pocs(self.W, self.H, pocs, sorted({r for v in rps.values() for r in v}),
+                                       self.qp, self.seed)
         up = lambda f: torch.from_numpy(f.view(np.int16)).to(self.device)  # noqa: E731
         d_recon = {p: up(f) for p, f in recon.items()}
         jobs = []
-        for poc in pocs:
-            rl = ref_list(poc)
-            jobs.append((up(orig[poc]), [d_recon[r] for r in rl], lambda_for_poc(self.qp, poc),
-                         self.eng.alloc_poc(len(rl), self.modes)))
+        for poc, refs in blocks:
+            jobs.append((up(orig[poc]), [d_recon[r] for r in rps[poc]], lambda_for_poc(self.qp, poc),
+                         self.eng.alloc_poc(len(refs), self.modes)))
         return jobs
 
     def step(self):
@@ -81,24 +83,26 @@ class ShardRun:
         return slabs, 4 * self.words * (self.world - 1)
 
     def verify(self, slabs, per_rank: int = 2):
-        """Rank 0: recompute up to `per_rank` POCs of every rank's block here
-        (first and last; a single-rank run recomputes its own) and compare their
-        records with the gathered slab, word for word."""
+        """Rank 0: recompute up to `per_rank` block entries of every rank (its
+        first and last POC, with that rank's refs; a single-rank run recomputes
+        its own) and compare their records with the gathered slab, word for
+        word."""
         checked, ok = [], True
         for r in range(self.world):
-            pocs = shard.poc_shard(self.n, self.world, r)
-            if not pocs:
+            blocks = shard.pair_shard(self.n, self.world, r)
+            if not blocks:
                 continue
-            sample = sorted({pocs[0], pocs[-1]})[:per_rank]
-            offs, o = {}, 0
-            for p in pocs:
-                offs[p] = o
-                o += shard.poc_words(len(ref_list(p)), self.modes, self.n_cus)
+            idx = sorted({0, len(blocks) - 1})[:per_rank]
+            offs, o = [], 0
+            for _, refs in blocks:
+                offs.append(o)
+                o += shard.poc_words(len(refs), self.modes, self.n_cus)
+            sample = [blocks[i] for i in idx]
             jobs = self._jobs(sample)
             self.eng.affine_me_batch(jobs, self.modes, 0)
-            for poc, job in zip(sample, jobs):
+            for i, (poc, refs), job in zip(idx, sample, jobs):
                 want = shard.pack([job[3]], None, self.device)
-                got = slabs[r][offs[poc]:offs[poc] + want.numel()]
+                got = slabs[r][offs[i]:offs[i] + want.numel()]
                 ok &= bool(torch.equal(got.to(want.device), want))
-                checked.append(poc)
+                checked.append([poc, refs])
         return {"pocs": checked, "byte_identical": ok}

@@ -1,12 +1,13 @@
 """Frame-shard multi-GPU plumbing.
 
-The hot path shards by POC: a (POC, ref) pair needs only orig[POC] and the
-recon frames named by the deterministic reference ring (main.cpp:591-707,
+The hot path shards by frame: a (POC, ref) pair needs only orig[POC] and the
+recon frame named by the deterministic reference ring (main.cpp:591-707,
 replayed by `hostlogic.ref_list` on every rank), and no result feeds another
-POC.  So every rank codes a contiguous block of POCs with no collective on the
-data path; the only exchange is the decision-log gather at the end (one
-all_gather of equal-size padded int32 slabs, RCCL over xGMI on the GPU box,
-gloo in the CPU tests).
+pair.  So every rank codes a contiguous block of the sequence's (POC, refIdx)
+pairs (`pair_shard`; `poc_shard` is the whole-POC cut) with no collective on
+the data path; the only exchange is the decision-log gather into rank 0 at the
+end (one gather of equal-size padded int32 slabs, RCCL over xGMI on the GPU
+box, gloo in the CPU tests).
 
 Decision records travel compacted, as int32 words: per (POC, ref, mode) the
 costs (one word each) followed by the mode's CPMV components ([n, 4] for
@@ -43,6 +44,42 @@ def poc_shard(n_frames: int, world: int, rank: int) -> list[int]:
         bounds.append(i)
     bounds.append(len(pocs))
     return pocs[bounds[rank]:bounds[rank + 1]]
+
+
+def pair_shard(n_frames: int, world: int, rank: int) -> list[tuple[int, list[int]]]:
+    """Contiguous block of the sequence's (POC, refIdx) pairs for `rank`, in
+    coding order (POC 1..n_frames, refIdx 0..min(4, POC)-1), as [(poc,
+    [refIdx, ...]), ...].  Every pair is an independent launch in the reference
+    (main.cpp:754-966, once per (POC, refIdx, PRED)), so the cut may fall inside
+    a POC; the blocks hold floor / ceil of total / world pairs each, so no rank
+    carries more than one pair above the mean (a POC-granular cut leaves up to a
+    whole 4-ref POC of imbalance: 6 vs 4 pairs at 2 ranks of 4 POCs)."""
+    pairs = [(p, r) for p in range(1, n_frames + 1) for r in range(pairs_per_poc(p))]
+    lo, hi = rank * len(pairs) // world, (rank + 1) * len(pairs) // world
+    blocks: list[tuple[int, list[int]]] = []
+    for p, r in pairs[lo:hi]:
+        if blocks and blocks[-1][0] == p:
+            blocks[-1][1].append(r)
+        else:
+            blocks.append((p, [r]))
+    return blocks
+
+
+def block_layout(blocks, modes: int, n_cus_per_align: tuple[int, int]):
+    """`unpack` / `slab_words` layout of a pair block (one entry per POC)."""
+    return [(len(refs), modes, n_cus_per_align) for _, refs in blocks]
+
+
+def merge_blocks(block_lists, results_lists) -> dict[int, dict]:
+    """Per-POC result dicts keyed by the true refIdx, from the unpacked results
+    of several ranks' pair blocks (a POC cut between two ranks is rejoined)."""
+    out: dict[int, dict] = {}
+    for blocks, results in zip(block_lists, results_lists):
+        for (poc, refs), res in zip(blocks, results):
+            d = out.setdefault(poc, {})
+            for (j, mode), v in res.items():
+                d[(refs[j], mode)] = v
+    return out
 
 
 def result_keys(nrefs: int, modes: int):
