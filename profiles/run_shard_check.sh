@@ -10,5 +10,5 @@ VAME_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnode
 python -c "
 import json
 for c in ('bench_default','c2_gloo2','c5_gloo2'):
-    d=json.load(open('$O/%s.json'%c)); print(c, d['ms_per_step'], d['value']/1e6, d['config']['pairs_per_step_rank0'], d['gather']['check'])
+    d=json.loads([l for l in open('$O/%s.json'%c) if l.startswith('{')][-1]); print(c, d['ms_per_step'], d['value']/1e6, d['config']['pairs_per_step_rank0'], d['gather']['check'])
 "
