@@ -654,7 +654,7 @@ int main(int argc, char** argv) {
   printf("Removing older outputs with identical names...\n");  // main.cpp:469 -> :1548
   vame_log_remove_old(prefix.c_str());
 
-  // ---- shard POCs 1..N over the devices: contiguous blocks balanced by pair count
+  // ---- shard POCs 1..N over the devices
   print_timestamp("START ALLOCATE MEMORY");
   const Layout L(nCtus);
   Shared S;
@@ -671,19 +671,13 @@ int main(int argc, char** argv) {
     s.owner = (int)(i / per_worker);
     S.pools[s.owner].push_back(&s);
   }
+  // Chunks of kBatchPocs consecutive POCs go to the devices in turn.  The writer
+  // takes POCs in order and each device holds at most per_worker unwritten
+  // slabs, so the devices must advance through the sequence together: with one
+  // contiguous block per device, device 1 would stall after its first
+  // per_worker POCs until the writer had drained device 0's whole block.
   std::vector<Job> jobs(ngpu);
-  {
-    long total = 0;
-    for (int p = 1; p <= N; p++) total += std::min(4, p);
-    long acc = 0;
-    int g = 0;
-    for (int p = 1; p <= N; p++) {
-      // move to the next device once this one holds its share of (POC, ref) pairs
-      if (g < ngpu - 1 && acc >= total * (g + 1) / ngpu) g++;
-      jobs[g].pocs.push_back(p);
-      acc += std::min(4, p);
-    }
-  }
+  for (int p = 1; p <= N; p++) jobs[((p - 1) / kBatchPocs) % ngpu].pocs.push_back(p);
   print_timestamp("FINISH ALLOCATE MEMORY");
 
   print_timestamp("START GPU KERNEL");
