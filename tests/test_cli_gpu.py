@@ -112,6 +112,20 @@ def test_cli_per_launch_and_two_workers_identical(seq416):
     compare_dirs(out2, exp)
 
 
+def test_cli_three_workers_chunk_dealing(tmp_path):
+    """--devices with 3 workers over 13 POCs: 4-POC chunks dealt in turn (POCs
+    1-4, 5-8, 9-12 to workers 0, 1, 2 and POC 13 back to worker 0), fused and
+    per-launch; the 40 logs equal the 1-worker run byte for byte."""
+    orig, recon = synth_sequence(416, 240, 13, qp=27, seed=3)
+    write_csv(str(tmp_path / "orig.csv"), orig)
+    write_csv(str(tmp_path / "recon.csv"), recon)
+    one, _ = run_cli(tmp_path, 416, 240, 13, 27, name="one")
+    assert len(compare_dirs(run_cli(tmp_path, 416, 240, 13, 27, ["--devices", "0,0,0"],
+                                    name="three")[0], one)) == 40
+    compare_dirs(run_cli(tmp_path, 416, 240, 13, 27, ["--devices", "0,0,0", "--per-launch"],
+                         name="three_pl")[0], one)
+
+
 def test_cli_align_selection(seq416):
     """--align full / half (SURVEY §8f CLI extension): each run launches one
     alignment's items only and writes exactly that alignment's files, byte
