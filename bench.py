@@ -14,8 +14,9 @@ QP32, 2 frames, 2-CPMV affine only (3 pairs, 196,425 candidate CUs per step).
 Multi-GPU (torchrun, one rank per GPU): every rank codes the
 contiguous (POC, refIdx) pair block shard.pair_shard(n, world, rank) of ONE sequence (the same
 synthetic seed on every rank), with no collective on the data path.
-  c2 / c3 / c4 scale weakly: the sequence has frames x N POCs, so every rank
-               codes about `frames` POCs (c2 at N = 1 is exactly configs[1]);
+  c2 / c3 / c4 scale weakly: the first P x N (POC, refIdx) pairs of the
+               sequence, P = the pairs of `frames` POCs, so every rank codes
+               exactly P pairs (c2: 3, c3 / c4: 114; at N = 1 exactly the config);
   c5           scales strongly: 240 POCs of 3840x2160 in all (configs[4]).
 After the timed steps the decision records go to rank 0 in one RCCL gather
 (timed and reported separately as `gather`), and rank 0 recomputes the first
@@ -100,10 +101,15 @@ def main():
     from vame.seqrun import ShardRun
 
     W, H, qp, modes = cfg["W"], cfg["H"], cfg["qp"], cfg["modes"]
-    n_frames = cfg["frames"] * (world if cfg["scaling"] == "weak" else 1)
+    # weak scaling: every rank codes exactly the pairs of the 1-GPU config (the
+    # first frames_pairs x N pairs of one sequence, cut at pair granularity);
+    # strong scaling: the config's whole sequence over the N ranks
+    from vame.shard import frames_for_pairs, sequence_pairs
+    n_pairs = sequence_pairs(cfg["frames"]) * world if cfg["scaling"] == "weak" else None
+    n_frames = frames_for_pairs(n_pairs) if n_pairs is not None else cfg["frames"]
     ncps = (2, 3) if modes & 2 else (2,)
     eng = Engine(W, H, dev.index)
-    run = ShardRun(eng, W, H, qp, n_frames, modes, world, rank, dev)
+    run = ShardRun(eng, W, H, qp, n_frames, modes, world, rank, dev, n_pairs=n_pairs)
     log(f"[rank {rank}] POCs {run.pocs[:1]}..{run.pocs[-1:]} ({run.pairs} pairs) of {n_frames}, "
         f"frames synthesized in {run.synth_s:.1f}s")
     acc = pair_accounting(W, H, ncps)
@@ -191,7 +197,8 @@ def main():
         "dtype": "int32",
         "data": "synthetic",
         "config": {"workload": cfg["label"], "resolution": f"{W}x{H}", "qp": qp,
-                   "sequence_frames": n_frames, "pocs_rank0": len(run.pocs),
+                   "sequence_frames": n_frames, "sequence_pairs": n_pairs or sequence_pairs(n_frames),
+                   "pocs_rank0": len(run.pocs),
                    "pairs_per_step_rank0": run.pairs, "rows_per_step_rank0": rows_per_step,
                    "rows_per_step_all": rows_total / args.steps,
                    "modes": "2cp+3cp" if modes & 2 else "2cp",

@@ -96,6 +96,24 @@ def test_pair_shard_covers_and_balances():
     assert shard.pair_shard(4, 2, 1) == [(3, [2]), (4, [0, 1, 2, 3])]
 
 
+def test_weak_scaling_prefix_fixed_pairs_per_rank():
+    """bench.py's weak scaling: the first P x N pairs of one sequence, P pairs
+    on every rank (c2: P = 3, c3 / c4: P = 114)."""
+    for frames in (2, 30):
+        P = shard.sequence_pairs(frames)
+        assert shard.frames_for_pairs(P) == frames
+        for world in (1, 2, 4, 8):
+            n = P * world
+            F = shard.frames_for_pairs(n)
+            assert shard.sequence_pairs(F) >= n > shard.sequence_pairs(F - 1)
+            blocks = [shard.pair_shard(F, world, r, n) for r in range(world)]
+            assert [sum(len(x) for _, x in b) for b in blocks] == [P] * world
+            flat = [(p, r) for b in blocks for p, refs in b for r in refs]
+            assert flat == [(p, r) for p in range(1, F + 1) for r in range(min(4, p))][:n]
+    with pytest.raises(ValueError):
+        shard.pair_shard(2, 1, 0, 4)
+
+
 def test_merge_blocks_rejoins_split_pocs():
     blocks = [shard.pair_shard(4, 2, r) for r in range(2)]
     res = [[{(j, "FULL_2CP"): (poc, refs[j]) for j in range(len(refs))} for poc, refs in b]

@@ -27,15 +27,16 @@ from .hostlogic import lambda_for_poc, ref_list
 
 
 class ShardRun:
-    """Pair block `pair_shard(n_frames, world, rank)` of the sequence
+    """Pair block `pair_shard(n_frames, world, rank, n_pairs)` of the sequence
     (W, H, qp, n_frames, seed), coded with `engine` on `device`."""
 
     def __init__(self, engine, W: int, H: int, qp: int, n_frames: int, modes: int, world: int,
-                 rank: int, device, seed: int = 0x5EED):
+                 rank: int, device, seed: int = 0x5EED, n_pairs: int | None = None):
         self.eng, self.W, self.H, self.qp, self.n = engine, W, H, qp, n_frames
+        self.n_pairs = n_pairs
         self.modes, self.world, self.rank, self.device, self.seed = modes, world, rank, device, seed
         self.n_cus = (engine.n_cus(0), engine.n_cus(1))
-        self.blocks = shard.pair_shard(n_frames, world, rank)
+        self.blocks = shard.pair_shard(n_frames, world, rank, n_pairs)
         self.pocs = [p for p, _ in self.blocks]
         t0 = time.perf_counter()
         self.jobs = self._jobs(self.blocks)
@@ -46,7 +47,8 @@ class ShardRun:
 
     def layout(self, rank: int):
         """`shard.unpack` layout of `rank`'s slab."""
-        return shard.block_layout(shard.pair_shard(self.n, self.world, rank), self.modes, self.n_cus)
+        return shard.block_layout(shard.pair_shard(self.n, self.world, rank, self.n_pairs), self.modes,
+                                  self.n_cus)
 
     def _jobs(self, blocks):
         """One engine job per (POC, [refIdx...]) entry; the job's results are
@@ -89,7 +91,7 @@ class ShardRun:
         word."""
         checked, ok = [], True
         for r in range(self.world):
-            blocks = shard.pair_shard(self.n, self.world, r)
+            blocks = shard.pair_shard(self.n, self.world, r, self.n_pairs)
             if not blocks:
                 continue
             idx = sorted({0, len(blocks) - 1})[:per_rank]

@@ -46,15 +46,35 @@ def poc_shard(n_frames: int, world: int, rank: int) -> list[int]:
     return pocs[bounds[rank]:bounds[rank + 1]]
 
 
-def pair_shard(n_frames: int, world: int, rank: int) -> list[tuple[int, list[int]]]:
+def sequence_pairs(n_frames: int) -> int:
+    """(POC, refIdx) pairs of a sequence of POC 1..n_frames."""
+    return sum(pairs_per_poc(p) for p in range(1, n_frames + 1))
+
+
+def frames_for_pairs(n_pairs: int) -> int:
+    """Fewest POCs whose sequence holds at least `n_pairs` pairs."""
+    f = 0
+    while sequence_pairs(f) < n_pairs:
+        f += 1
+    return f
+
+
+def pair_shard(n_frames: int, world: int, rank: int,
+               n_pairs: int | None = None) -> list[tuple[int, list[int]]]:
     """Contiguous block of the sequence's (POC, refIdx) pairs for `rank`, in
     coding order (POC 1..n_frames, refIdx 0..min(4, POC)-1), as [(poc,
-    [refIdx, ...]), ...].  Every pair is an independent launch in the reference
-    (main.cpp:754-966, once per (POC, refIdx, PRED)), so the cut may fall inside
-    a POC; the blocks hold floor / ceil of total / world pairs each, so no rank
-    carries more than one pair above the mean (a POC-granular cut leaves up to a
-    whole 4-ref POC of imbalance: 6 vs 4 pairs at 2 ranks of 4 POCs)."""
+    [refIdx, ...]), ...].  Every pair is an independent launch in the
+    reference (main.cpp:754-966, once per (POC, refIdx, PRED)), so the cut may
+    fall inside a POC; the blocks hold floor / ceil of total / world pairs each,
+    so no rank carries more than one pair above the mean (a POC-granular cut
+    leaves up to a whole 4-ref POC of imbalance: 6 vs 4 pairs at 2 ranks of 4
+    POCs).  `n_pairs` keeps only the sequence's first n_pairs pairs (weak
+    scaling at a fixed pair count per rank)."""
     pairs = [(p, r) for p in range(1, n_frames + 1) for r in range(pairs_per_poc(p))]
+    if n_pairs is not None:
+        if n_pairs > len(pairs):
+            raise ValueError("n_pairs exceeds the sequence's pairs")
+        pairs = pairs[:n_pairs]
     lo, hi = rank * len(pairs) // world, (rank + 1) * len(pairs) // world
     blocks: list[tuple[int, list[int]]] = []
     for p, r in pairs[lo:hi]:
