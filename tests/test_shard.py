@@ -1,7 +1,7 @@
 """Multi-process (gloo, world_size 2, CPU) test of the frame-shard path of
 SURVEY.md §8e: every rank codes its contiguous POC block (`poc_shard`) or pair
-block (`pair_shard`, bench.py's path), the decision records travel in one gather, and rank 0's reassembled log equals the
-single-process run.  The per-pair compute here is the CPU oracle (this is a
+block (`pair_shard`, bench.py's path), the decision records travel in one
+collective, and rank 0's reassembled log equals the single-process run.  The per-pair compute here is the CPU oracle (this is a
 test of the sharding and exchange plumbing; the GPU path is covered by
 test_gpu_parity.py)."""
 import os
