@@ -11,7 +11,11 @@ where the config asks for it), inputs resident in HBM, in one
 vame_affine_me_batch call.  Default = BASELINE.json configs[1]: 1920x1080
 QP32, 2 frames, 2-CPMV affine only (3 pairs, 196,425 candidate CUs per step).
 
-Multi-GPU (torchrun, one rank per GPU): every rank codes the
+Multi-GPU (one rank per GPU): `--gpus N` starts the N ranks
+itself (fresh child processes, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+started before anything touches the GPU; backend nccl = RCCL over xGMI, or
+VAME_DIST_BACKEND=gloo to rehearse several ranks on one GPU); under a launcher
+(torchrun) that set WORLD_SIZE, WORLD_SIZE must equal --gpus.  Every rank codes the
 contiguous (POC, refIdx) pair block shard.pair_shard(n, world, rank) of ONE sequence (the same
 synthetic seed on every rank), with no collective on the data path.
   c2 / c3 / c4 scale weakly: the first P x N (POC, refIdx) pairs of the
@@ -77,24 +81,18 @@ def main():
     if args.frames is not None:
         cfg["frames"] = args.frames
 
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    from vame.launch import init_rank, launch_ranks
+    backend = os.environ.get("VAME_DIST_BACKEND", "nccl")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:  # no launcher: start the N ranks here (nothing has touched the GPU yet)
+            sys.exit(launch_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:], backend,
+                                  "bench.py"))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher but --gpus {args.gpus}")
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        # one rank per GPU over RCCL; VAME_DIST_BACKEND=gloo rehearses the
-        # multi-rank path with several ranks on one GPU (the driver's runs use RCCL)
-        backend = os.environ.get("VAME_DIST_BACKEND", "nccl")
-        local = local % torch.cuda.device_count() if backend != "nccl" else local
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dist, rank, dev = init_rank(world, backend)
 
     from vame.engine import Engine
     from vame.metrics import pair_accounting
@@ -138,11 +136,16 @@ def main():
         run.step()
     barrier()
     eng.set_timing(True)
+    # one event per step boundary on the issuing stream: the per-step spread
+    step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t_start = time.perf_counter()
-    for _ in range(args.steps):
+    step_ev[0].record()
+    for i in range(args.steps):
         run.step()
+        step_ev[i + 1].record()
     barrier()
     elapsed = time.perf_counter() - t_start
+    step_ms = sorted(step_ev[i].elapsed_time(step_ev[i + 1]) for i in range(args.steps))
     quad_ms, quad_n = eng.get_timing(0)
     big_ms, big_n = eng.get_timing(1)
     eng.set_timing(False)
@@ -191,6 +194,10 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": tmax * 1e3 / args.steps,
+        # rank 0's per-step GPU times (HIP events at the step boundaries)
+        "step_ms": {"median": step_ms[len(step_ms) // 2], "min": step_ms[0], "max": step_ms[-1]},
+        "world": {"size": world, "backend": "none" if dist is None else dist.get_backend(),
+                  "launcher": os.environ.get("VAME_LAUNCHER", "external" if world > 1 else "none")},
         "higher_is_better": True,
         "scaling": cfg["scaling"],
         "vs_baseline": None,

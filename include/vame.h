@@ -138,6 +138,10 @@ int vame_ref_list(int poc, int* pocs);
  * Returns 0, or VAME_E_INVALID for a missing file / short file / bad value. */
 int vame_read_frames(const char* path, int width, int height, int nframes, uint16_t* out,
                      int nthreads);
+/* The same for frames first .. first + nframes - 1 of the file (a frame-sharded
+ * rank reads only the frames its POC block uses). */
+int vame_read_frames_range(const char* path, int width, int height, int first, int nframes,
+                           uint16_t* out, int nthreads);
 
 /* Decision log (main_aux_functions.h:387-525, 1547-1585).  pred = 0 FULL_2CP,
  * 1 FULL_3CP, 2 HALF_2CP, 3 HALF_3CP (constants.h:15-21).  Files are
@@ -169,6 +173,11 @@ typedef struct vame_log_writer vame_log_writer;
 vame_log_writer* vame_log_writer_create(const char* prefix, int width, int height, int nthreads);
 long long vame_log_writer_poc(vame_log_writer* w, int poc, int nrefs, int pred_mask,
                               const int64_t* const* cost, const vame_cpmvs* const* cpmvs);
+/* The same for refIdx ref0 .. ref0 + nrefs - 1 only (arrays indexed
+ * (r - ref0)*4 + m): a POC whose refIdx range is cut between two frame-shard
+ * ranks is logged by each for its own refs, in the same order. */
+long long vame_log_writer_refs(vame_log_writer* w, int poc, int ref0, int nrefs, int pred_mask,
+                               const int64_t* const* cost, const vame_cpmvs* const* cpmvs);
 int vame_log_writer_destroy(vame_log_writer* w);
 
 const char* vame_strerror(int code);

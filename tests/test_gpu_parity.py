@@ -136,27 +136,50 @@ REF_HARNESS = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle",
 
 @pytest.mark.skipif(not os.path.exists(REF_HARNESS), reason="reference kernels not built")
 def test_live_reference_1080p(engines, tmp_path):
-    """The reference kernels themselves, run on this GPU, vs the HIP path at 1080p."""
+    """The reference kernels themselves, run on this GPU, vs the HIP path at 1080p.
+
+    The reference hands gradients and equations between work-items through
+    global memory behind only a local barrier (affine.cl:487-514, 715-738), so
+    one of its runs can race.  As in the golden pipeline (make_golden.py
+    pack), the reference runs twice and its output counts only if both runs
+    agree bit for bit; if they do not, the HIP path is checked against the
+    oracle instead and the test reports the reference-side race as an xfail."""
     from vame import synth
     o, r = synth.synth_sequence(1920, 1080, 1, 32, seed=0xABCD)
     lam = 78.949063
     r[0].tofile(tmp_path / "ref.u16")
     o[0].tofile(tmp_path / "cur.u16")
-    (tmp_path / "jobs.txt").write_text(
-        f"1920 1080 {lam!r} 0 {tmp_path / 'ref.u16'} {tmp_path / 'cur.u16'} {tmp_path / 'p'}\n")
     d = os.path.dirname(REF_HARNESS)
-    subprocess.run([REF_HARNESS, os.path.join(d, "affine_2cp.co"), os.path.join(d, "affine_3cp.co"),
-                    str(tmp_path / "jobs.txt")], check=True, timeout=300, capture_output=True)
+    runs = []
+    for tag in ("A", "B"):
+        (tmp_path / f"jobs_{tag}.txt").write_text(
+            f"1920 1080 {lam!r} 0 {tmp_path / 'ref.u16'} {tmp_path / 'cur.u16'} {tmp_path / tag}\n")
+        subprocess.run([REF_HARNESS, os.path.join(d, "affine_2cp.co"), os.path.join(d, "affine_3cp.co"),
+                        str(tmp_path / f"jobs_{tag}.txt")], check=True, timeout=300, capture_output=True)
+        res = {}
+        for name in MODES:
+            n = 135 * (201 if name.startswith("FULL") else 284)
+            raw = np.fromfile(tmp_path / f"{tag}_{name}.bin", np.uint8)
+            res[name] = (raw[:n * 8].view(np.int64), raw[n * 8:].view(np.int32).reshape(n, 7)[:, 1:])
+        runs.append(res)
     eng = engines(1920, 1080)
     out = eng.affine_me_poc(dev(o[0]), [dev(r[0])], lam, modes=3)
+    racy = [name for name in MODES if not (np.array_equal(runs[0][name][0], runs[1][name][0])
+                                           and np.array_equal(runs[0][name][1], runs[1][name][1]))]
+    if racy:
+        want = O.affine_me_pair(r[0], o[0], lam)
+        for name, key in zip(MODES, ((0, 2), (0, 3), (1, 2), (1, 3))):
+            hc, hp = host(out[(0, name)])
+            oc, op = want[key]
+            np.testing.assert_array_equal(hc, oc, err_msg=name)
+            np.testing.assert_array_equal(cp6(hp), oracle_cp6(op), err_msg=name)
+        pytest.xfail(f"reference runs disagree (its global-memory race, affine.cl:487-514 / "
+                     f"715-738) on {racy}; the HIP path equals the oracle")
     for name in MODES:
-        n = 135 * (201 if name.startswith("FULL") else 284)
-        raw = np.fromfile(tmp_path / f"p_{name}.bin", np.uint8)
-        cost = raw[:n * 8].view(np.int64)
-        cp = raw[n * 8:].view(np.int32).reshape(n, 7)
+        cost, cp = runs[0][name]
         hc, hp = host(out[(0, name)])
         np.testing.assert_array_equal(hc, cost, err_msg=name)
-        np.testing.assert_array_equal(cp6(hp), cp[:, 1:], err_msg=name)
+        np.testing.assert_array_equal(cp6(hp), cp, err_msg=name)
 
 
 PROF_CASES = [p for p in GOLDEN if any(k in p for k in ("qp32_poc1", "bigmotion", "extra1", "s832"))]

@@ -289,3 +289,94 @@ def test_pred_mask_mirrors_the_abi():
     masks = (1, 3, 5, 7, 9, 11, 13, 15)
     assert [pred_mask(m) for m in masks] == [5, 15, 1, 3, 4, 12, 5, 15]
     assert [logs.lib().vame_pred_mask(m) for m in masks] == [pred_mask(m) for m in masks]
+
+
+def _random_poc(rng, W, H, refs, preds=range(4)):
+    n_ctus = logs.lib().vame_num_ctus(W, H)
+    res = {}
+    for r in refs:
+        for m in preds:
+            n = n_ctus * (284 if m >> 1 else 201)
+            res[(r, logs.PREDS[m])] = (rng.integers(0, 1 << 31, n),
+                                       rng.integers(-70000, 70000, (n, 7)).astype(np.int32))
+    return res
+
+
+def test_log_append_concurrent_threads(tmp_path):
+    """vame_log_append from two threads at once (ctypes drops the GIL): each
+    call runs its own threads, so both logs equal a serial run."""
+    import threading
+    rng = np.random.default_rng(5)
+    res = [_random_poc(rng, 1920, 1080, [0]) for _ in range(2)]
+    def job(k, d, reps):
+        for _ in range(reps):
+            for m, name in enumerate(logs.PREDS):
+                logs.append(str(d / f"log{k}"), m, 1920, 1080, 1, 0, *res[k][(0, name)], nthreads=4)
+    par, ser = tmp_path / "par", tmp_path / "ser"
+    par.mkdir()
+    ser.mkdir()
+    th = [threading.Thread(target=job, args=(k, par, 3)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for k in range(2):
+        job(k, ser, 3)
+    fa = _files(par)
+    assert fa == _files(ser) and len(fa) == 80
+    for f in fa:
+        assert (par / f).read_bytes() == (ser / f).read_bytes(), f
+
+
+def test_log_writer_refs_and_fork(tmp_path):
+    """vame_log_writer_refs (a POC's refIdx range cut between frame-shard
+    ranks): the two halves written one after the other equal the whole POC;
+    and a writer whose pool started before a fork() still works in the child
+    (serially) instead of waiting for threads the child does not have."""
+    rng = np.random.default_rng(8)
+    res = _random_poc(rng, 416, 240, range(4))
+    a, b = tmp_path / "whole", tmp_path / "halves"
+    a.mkdir()
+    b.mkdir()
+    with logs.LogWriter(str(a / "log"), 416, 240, nthreads=3) as w:
+        w.poc(7, res)
+    with logs.LogWriter(str(b / "log"), 416, 240, nthreads=3) as w:
+        w.poc(7, {k: v for k, v in res.items() if k[0] < 1})
+        w.poc(7, {k: v for k, v in res.items() if k[0] >= 1})
+    for f in _files(a):
+        assert (a / f).read_bytes() == (b / f).read_bytes(), f
+    with pytest.raises(ValueError):
+        logs.LogWriter(str(b / "bad"), 416, 240).poc(7, {k: v for k, v in res.items() if k[0] != 1})
+    c = tmp_path / "forked"
+    c.mkdir()
+    w = logs.LogWriter(str(c / "log"), 416, 240, nthreads=4)
+    w.poc(7, {k: v for k, v in res.items() if k[0] < 1})  # pool threads are running now
+    pid = os.fork()
+    if pid == 0:  # child: finish the POC with the inherited writer, then leave at once
+        try:
+            w.poc(7, {k: v for k, v in res.items() if k[0] >= 1})
+            w.close()
+            os._exit(0)
+        except BaseException:
+            os._exit(1)
+    _, status = os.waitpid(pid, 0)
+    assert os.waitstatus_to_exitcode(status) == 0
+    for f in _files(a):
+        assert (a / f).read_bytes() == (c / f).read_bytes(), f
+    w._w = None  # the parent's copy: its files were completed by the child
+
+
+def test_read_frames_range(tmp_path):
+    """vame_read_frames_range: frames first .. first+n-1 of a CSV / raw file
+    (a frame-sharded rank's share), equal to the slice of a whole read."""
+    rng = np.random.default_rng(3)
+    fr = rng.integers(0, 1024, size=(5, 240, 416)).astype(np.uint16)
+    p = str(tmp_path / "f.csv")
+    write_csv(p, fr)
+    fr.tofile(str(tmp_path / "f.u16"))
+    for path in (p, str(tmp_path / "f.u16")):
+        for first, n in ((0, 5), (2, 3), (4, 1), (1, 2)):
+            for t in (1, 5):
+                assert (logs.read_frames(path, 416, 240, n, t, first=first) == fr[first:first + n]).all()
+        with pytest.raises(logs.VameError):
+            logs.read_frames(path, 416, 240, 2, first=4)

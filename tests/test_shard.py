@@ -145,6 +145,39 @@ def test_pack_unpack_roundtrip():
             assert torch.equal(a[k][0], b[k][0]) and torch.equal(a[k][1], b[k][1])
 
 
+def test_pack_unpack_alignment_selection():
+    """Mode masks with a FULL / HALF selection (vame_pred_mask): pack writes
+    only the selected PREDs and unpack expects exactly those; a result set that
+    does not match the mask is refused instead of being decoded at the wrong
+    offsets."""
+    from vame.engine import MODE_2CP, MODE_3CP, MODE_FULL, MODE_HALF
+    g = torch.Generator().manual_seed(2)
+    n = {"FULL": 10, "HALF": 12}
+    def rec(m):
+        ncp = 3 if m.endswith("3CP") else 2
+        cp = torch.randint(-2**17, 2**17, (n[m[:4]], 7), dtype=torch.int32, generator=g)
+        cp[:, 0] = ncp
+        if ncp == 2:
+            cp[:, 5:] = 0
+        return torch.randint(0, 2**31, (n[m[:4]],), dtype=torch.int64, generator=g), cp
+    for modes, names in ((MODE_2CP | MODE_HALF, ("HALF_2CP",)),
+                         (MODE_2CP | MODE_3CP | MODE_HALF, ("HALF_2CP", "HALF_3CP")),
+                         (MODE_2CP | MODE_FULL, ("FULL_2CP",)),
+                         (MODE_2CP | MODE_3CP, shard.MODES)):
+        assert [k for k in shard.result_keys(1, modes)] == [(0, m) for m in names]
+        res = [{(r, m): rec(m) for r in range(nr) for m in names} for nr in (2, 1)]
+        lay = [(2, modes, (10, 12)), (1, modes, (10, 12))]
+        flat = shard.pack(res, shard.slab_words(lay), modes=modes)
+        back = shard.unpack(flat, lay)
+        for a, b in zip(res, back):
+            assert sorted(a) == sorted(b)
+            for k in a:
+                assert torch.equal(a[k][0], b[k][0]) and torch.equal(a[k][1], b[k][1])
+    with pytest.raises(ValueError):
+        shard.pack([{(0, "FULL_2CP"): rec("FULL_2CP"), (0, "HALF_2CP"): rec("HALF_2CP")}],
+                   modes=MODE_2CP | MODE_HALF)
+
+
 @pytest.mark.timeout(300)
 def test_two_rank_gather_equals_single_process(tmp_path):
     port = free_port()
@@ -259,7 +292,8 @@ def bench_path_worker(rank, world, port, outdir):
     slabs, nbytes = run.gather()
     if rank == 0:
         check = run.verify(slabs)
-        torch.save({"slabs": slabs, "check": check, "bytes": nbytes, "pocs": run.pocs},
+        full = run.verify(slabs, full=True)
+        torch.save({"slabs": slabs, "check": check, "full": full, "bytes": nbytes, "pocs": run.pocs},
                    os.path.join(outdir, "bench_path.pt"))
     else:
         assert slabs is None
@@ -278,6 +312,10 @@ def test_bench_shard_path_two_ranks_equals_single_process(tmp_path):
     mp.spawn(bench_path_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     got = torch.load(os.path.join(tmp_path, "bench_path.pt"), weights_only=True)
     assert got["check"]["byte_identical"] and len(got["check"]["pocs"]) >= 3
+    # POC 4 is cut (rank 0: refIdx 0, rank 1: refIdx 1-3): both halves recomputed
+    assert got["check"]["cut_pocs"] == [4]
+    assert [4, [0], 0] in got["check"]["pocs"] and [4, [1, 2, 3], 1] in got["check"]["pocs"]
+    assert got["full"]["byte_identical"] and len(got["full"]["pocs"]) == 6  # every block entry
     single = ShardRun(OracleEngine(SEQ_W, SEQ_H), SEQ_W, SEQ_H, 27, SEQ_N, 3, 1, 0,
                       torch.device("cpu"), seed=11)
     single.step()

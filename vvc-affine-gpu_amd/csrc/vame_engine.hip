@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -38,6 +39,9 @@ struct vame_ctx {
   Item* dQuad = nullptr;
   Item* dBig = nullptr;
   int nQuadFull = 0, nQuadHalf = 0, nBig = 0;
+  // block order (block_grid): slot -> CTU table, CTU chunks, slots per (pair, chunk)
+  int32_t* dOrder = nullptr;
+  int groupCombos = 408, nChunks = 1, cpp = 0;
   hipStream_t side = nullptr;   // second stream: 128-class items run beside the quadrant items
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   // optional per-kernel timing: (start, end) event pairs per kernel class
@@ -246,18 +250,62 @@ struct DeviceGuard {
     if (rc_) return rc_;   \
   } while (0)
 
-// Block order (affine_me_body): pairs in groups of about kGroupCombos (ctu,
-// pair) combinations -- the 3 pairs of a 1080p 2-frame step, whose tiles and
-// original samples the XCDs' L2s hold while every item of a CTU passes -- and
-// within a group, (ctu, pair) combinations per template item padded to a
-// multiple of 8 (one per XCD) so every item of a CTU lands on the same XCD
-// (padding blocks exit at once).  Returns the grid size.
-constexpr int kGroupCombos = 408;
-unsigned block_grid(KParams& k) {
-  k.groupPairs = std::max(1, std::min(k.nPairs, kGroupCombos / k.nCtus));
-  k.groupPer = (k.nCtus * k.groupPairs + 7) / 8 * 8;
-  const int groups = (k.nPairs + k.groupPairs - 1) / k.groupPairs;
+// Block order (affine_me_body): groups of about c->groupCombos (ctu, pair)
+// combinations, whose tiles and original samples the XCDs' L2s hold while
+// every item of a CTU passes -- the 3 pairs of a 1080p 2-frame step, or one
+// chunk of CTU rows of one 2160p pair -- and within a group, the (ctu, pair)
+// combinations of each template item in slots padded to a multiple of 8 per
+// (pair, chunk), so every item of a CTU lands on the same XCD (padding blocks
+// exit at once).  Returns the grid size.
+unsigned block_grid(const vame_ctx* c, KParams& k) {
+  k.order = c->dOrder;
+  k.nChunks = c->nChunks;
+  k.cpp = c->cpp;
+  k.groupPairs = c->nChunks > 1 ? 1 : std::max(1, std::min(k.nPairs, c->groupCombos / c->cpp));
+  k.groupPer = k.groupPairs * c->cpp;
+  const int groups = (k.nPairs + k.groupPairs - 1) / k.groupPairs * c->nChunks;
   return (unsigned)(groups * k.nItems * k.groupPer);
+}
+
+// The slot -> CTU table of the block order: the frame's CTU rows cut into
+// chunks of at most groupCombos CTUs; within a chunk, slot j runs on XCD j % 8
+// (workgroups are dealt round-robin over the XCDs), and with xcdOrder = 1 XCD
+// x takes the x-th eighth of the chunk's CTUs in column-major order -- a
+// compact strip, so the margins of neighbouring reference tiles hit that
+// XCD's L2 -- while xcdOrder = 0 deals the CTUs in raster order.
+std::vector<int32_t> build_order(int nCtus, int cols, int groupCombos, int xcdOrder, int& nChunks,
+                                 int& cpp) {
+  const int rows = nCtus / cols;
+  nChunks = (nCtus + groupCombos - 1) / groupCombos;
+  const int rowsPer = (rows + nChunks - 1) / nChunks;
+  nChunks = (rows + rowsPer - 1) / rowsPer;
+  const int seg = (rowsPer * cols + 7) / 8;
+  cpp = seg * 8;
+  std::vector<int32_t> order((size_t)nChunks * cpp, -1);
+  for (int ch = 0; ch < nChunks; ch++) {
+    const int r0 = ch * rowsPer, r1 = std::min(rows, r0 + rowsPer);
+    std::vector<int> L;
+    if (xcdOrder)
+      for (int x = 0; x < cols; x++)
+        for (int y = r0; y < r1; y++) L.push_back(y * cols + x);
+    else
+      for (int y = r0; y < r1; y++)
+        for (int x = 0; x < cols; x++) L.push_back(y * cols + x);
+    int32_t* o = order.data() + (size_t)ch * cpp;
+    if (xcdOrder) {
+      const int s = ((int)L.size() + 7) / 8;  // CTUs per XCD in this chunk
+      for (int x = 0; x < 8; x++)
+        for (int i = 0; i < s && x * s + i < (int)L.size(); i++) o[8 * i + x] = L[x * s + i];
+    } else {
+      for (size_t j = 0; j < L.size(); j++) o[j] = L[j];
+    }
+  }
+  return order;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
 }
 
 // The kernel instance of a launch mode (vame_kernel.h MODE: 1 = 2-CP only,
@@ -298,7 +346,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     KParams kb = kp;
     kb.items = c->dBig;
     kb.nItems = c->nBig;
-    const unsigned grid = block_grid(kb);
+    const unsigned grid = block_grid(c, kb);
     VAME_TRY(time_begin(c, 1, sBig));
     hipLaunchKernelGGL(kernel_for<true>(c->prof, mode), dim3(grid),
                        dim3(Cfg<128>::THREADS), 0, sBig, kb);
@@ -310,7 +358,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     KParams kq = kp;
     kq.items = quadFull ? c->dQuad : c->dQuad + c->nQuadFull;
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
-    const unsigned grid = block_grid(kq);
+    const unsigned grid = block_grid(c, kq);
     VAME_TRY(time_begin(c, 0, sQuad));
     hipLaunchKernelGGL(kernel_for<false>(c->prof, mode), dim3(grid),
                        dim3(Cfg<64>::THREADS), 0, sQuad, kq);
@@ -387,7 +435,14 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   c->nQuadHalf = (int)qh.size();
   std::vector<Item> quad(qf);
   quad.insert(quad.end(), qh.begin(), qh.end());
+  // tuning knobs of the block order (defaults measured on MI355X)
+  c->groupCombos = std::max(8, env_int("VAME_GROUP_COMBOS", 408));
+  const std::vector<int32_t> order = build_order(nCtus, c->ctusPerRow, c->groupCombos,
+                                                 env_int("VAME_XCD_ORDER", 1), c->nChunks, c->cpp);
   hipError_t e = hipMalloc(&c->dQuad, quad.size() * sizeof(Item));
+  if (e == hipSuccess) e = hipMalloc(&c->dOrder, order.size() * sizeof(int32_t));
+  if (e == hipSuccess)
+    e = hipMemcpy(c->dOrder, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&c->dBig, big.size() * sizeof(Item));
   if (e == hipSuccess) e = hipMemcpy(c->dQuad, quad.data(), quad.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->dBig, big.data(), big.size() * sizeof(Item), hipMemcpyHostToDevice);
@@ -408,6 +463,7 @@ void vame_destroy(vame_ctx* c) {
   DeviceGuard guard(c->device);
   if (c->dQuad) (void)hipFree(c->dQuad);
   if (c->dBig) (void)hipFree(c->dBig);
+  if (c->dOrder) (void)hipFree(c->dOrder);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->evFork) (void)hipEventDestroy(c->evFork);
   if (c->evJoin) (void)hipEventDestroy(c->evJoin);

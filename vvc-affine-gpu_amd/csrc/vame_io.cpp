@@ -75,31 +75,38 @@ int pick_threads(int requested, long work_items) {
 }
 
 // Persistent workers for the log writer: run(n, f) calls f(i) for i < n on
-// the workers and the calling thread, and returns when all are done.
+// the workers and the calling thread, and returns when all are done.  Callers
+// on several threads take turns (run_mu_); in a child forked after the pool
+// started -- which has none of its threads -- run() works serially; the
+// owner must not destroy a pool there (forked(): its condition variables
+// still count the parent's waiting threads, and destroying them would wait
+// for those forever), and leaks it instead.
 class Pool {
  public:
-  explicit Pool(int nthreads) {
-    for (int t = 1; t < nthreads; t++) th_.emplace_back([this] { loop(); });
+  explicit Pool(int nthreads) : pid_(getpid()), th_(new std::vector<std::thread>) {
+    for (int t = 1; t < nthreads; t++) th_->emplace_back([this] { loop(); });
   }
+  bool forked() const { return getpid() != pid_; }
   ~Pool() {
     {
       std::lock_guard<std::mutex> g(mu_);
       stop_ = true;
     }
     cv_.notify_all();
-    for (auto& t : th_) t.join();
+    for (auto& t : *th_) t.join();
   }
   void run(int n, const std::function<void(int)>& f) {
-    if (th_.empty() || n <= 1) {
+    if (th_->empty() || n <= 1 || forked()) {
       for (int i = 0; i < n; i++) f(i);
       return;
     }
+    std::lock_guard<std::mutex> turn(run_mu_);
     {
       std::lock_guard<std::mutex> g(mu_);
       job_ = &f;
       n_ = n;
       next_.store(0);
-      active_ = (int)th_.size();
+      active_ = (int)th_->size();
       gen_++;
     }
     cv_.notify_all();
@@ -127,8 +134,9 @@ class Pool {
       if (--active_ == 0) done_.notify_all();
     }
   }
-  std::vector<std::thread> th_;
-  std::mutex mu_;
+  const pid_t pid_;
+  std::unique_ptr<std::vector<std::thread>> th_;
+  std::mutex mu_, run_mu_;
   std::condition_variable cv_, done_;
   const std::function<void(int)>* job_ = nullptr;
   int n_ = 0, active_ = 0;
@@ -331,22 +339,6 @@ void format_rows(Buf& buf, int align, int g, int ctu0, int ctu1, int ctuCols, in
   buf.len = (size_t)(p - p0);
 }
 
-// Process-wide pool of the per-call entry points (vame_log_append,
-// vame_read_frames keep their own threads): sized on first use.
-Pool& shared_pool(int nthreads) {
-  static std::mutex mu;
-  static std::unique_ptr<Pool> pool;
-  static int size = 0;
-  std::lock_guard<std::mutex> g(mu);
-  const int want = pick_threads(nthreads, 1 << 20);
-  if (!pool || size != want) {
-    pool.reset();
-    pool.reset(new Pool(want));
-    size = want;
-  }
-  return *pool;
-}
-
 }  // namespace
 
 // A POC-at-a-time decision-log writer (include/vame.h vame_log_writer_*).
@@ -363,6 +355,7 @@ struct vame_log_writer {
   ~vame_log_writer() {
     for (int fd : fds)
       if (fd >= 0) close(fd);
+    if (pool && pool->forked()) (void)pool.release();  // see Pool: leaked in a forked child
   }
 };
 
@@ -403,7 +396,13 @@ vame_log_writer* vame_log_writer_create(const char* prefix, int width, int heigh
 
 long long vame_log_writer_poc(vame_log_writer* w, int poc, int nrefs, int pred_mask,
                               const int64_t* const* cost, const vame_cpmvs* const* cpmvs) {
-  if (!w || nrefs <= 0 || nrefs > 4 || !cost || !cpmvs || (pred_mask & ~15)) return VAME_E_INVALID;
+  return vame_log_writer_refs(w, poc, 0, nrefs, pred_mask, cost, cpmvs);
+}
+
+long long vame_log_writer_refs(vame_log_writer* w, int poc, int ref0, int nrefs, int pred_mask,
+                               const int64_t* const* cost, const vame_cpmvs* const* cpmvs) {
+  if (!w || ref0 < 0 || nrefs <= 0 || ref0 + nrefs > 4 || !cost || !cpmvs || (pred_mask & ~15))
+    return VAME_E_INVALID;
   for (int r = 0; r < nrefs; r++)
     for (int m = 0; m < 4; m++)
       if (((pred_mask >> m) & 1) && (!cost[r * 4 + m] || !cpmvs[r * 4 + m])) return VAME_E_INVALID;
@@ -424,7 +423,7 @@ long long vame_log_writer_poc(vame_log_writer* w, int poc, int nrefs, int pred_m
   w->pool->run((int)tasks.size(), [&](int i) {
     const Task& t = tasks[i];
     format_rows(w->bufs[i], t.m >> 1, t.g, t.c * kLogChunk, std::min(w->nCtus, (t.c + 1) * kLogChunk),
-                w->ctuCols, poc, t.r, cost[t.r * 4 + t.m], cpmvs[t.r * 4 + t.m]);
+                w->ctuCols, poc, ref0 + t.r, cost[t.r * 4 + t.m], cpmvs[t.r * 4 + t.m]);
   });
   // per file, its tasks in order (a file belongs to one PRED; HALF names
   // shared by several groups take them in group order, as the reference's
@@ -489,17 +488,25 @@ int vame_log_writer_destroy(vame_log_writer* w) {
 
 int vame_read_frames(const char* path, int width, int height, int nframes, uint16_t* out,
                      int nthreads) {
-  if (!path || !out || width <= 0 || height <= 0 || nframes <= 0) return VAME_E_INVALID;
+  return vame_read_frames_range(path, width, height, 0, nframes, out, nthreads);
+}
+
+int vame_read_frames_range(const char* path, int width, int height, int first_frame, int nframes,
+                           uint16_t* out, int nthreads) {
+  const int first = first_frame;
+  if (!path || !out || width <= 0 || height <= 0 || first < 0 || nframes <= 0) return VAME_E_INVALID;
   Mapped m;
   int rc = map_file(path, m);
   if (rc) return rc;
   const size_t fsz = (size_t)width * height;
   if (ends_with(path, ".u16") || ends_with(path, ".yuv")) {  // raw 16-bit side path
-    if (m.n < fsz * nframes * 2) return VAME_E_INVALID;
-    memcpy(out, m.p, fsz * nframes * 2);
+    if (m.n < fsz * ((size_t)first + nframes) * 2) return VAME_E_INVALID;
+    memcpy(out, m.p + fsz * first * 2, fsz * nframes * 2);
     return VAME_OK;
   }
-  const long nlines = (long)nframes * height;
+  // text lines [line0, nlines) are frames first .. first + nframes - 1
+  const long line0 = (long)first * height;
+  const long nlines = ((long)first + nframes) * height;
   const char* base = m.p;
   const size_t n = m.n;
   if (n == 0) return VAME_E_INVALID;
@@ -519,28 +526,28 @@ int vame_read_frames(const char* path, int width, int height, int nframes, uint1
     nl[t] = c;
   });
   // line index of the first line starting in range t: lines start at 0 and after each '\n'
-  std::vector<long> first(T + 1, 0);
-  for (int t = 0; t < T; t++) first[t + 1] = first[t] + nl[t];
-  const long total_lines = first[T] + (base[n - 1] != '\n' ? 1 : 0);
+  std::vector<long> firstLine(T + 1, 0);
+  for (int t = 0; t < T; t++) firstLine[t + 1] = firstLine[t] + nl[t];
+  const long total_lines = firstLine[T] + (base[n - 1] != '\n' ? 1 : 0);
   if (total_lines < nlines) return VAME_E_INVALID;
   // pass 2: parse the lines that START in each range (line 0 starts at byte 0)
   std::vector<int> bad(T, 0);
   parallel_for(T, T, [&](int t, int) {
     const char* q = base + cut[t];
-    long li = first[t];
+    long li = firstLine[t];
     if (t > 0) {  // skip the tail of a line started in an earlier range
       if (base[cut[t] - 1] != '\n') {
         const char* r = (const char*)memchr(q, '\n', (size_t)(base + cut[t + 1] - q));
         if (!r) return;
         q = r + 1;
-        li++;  // first[t] is the line that straddles cut[t]; q starts the next one
+        li++;  // firstLine[t] is the line that straddles cut[t]; q starts the next one
       }
     }
     const char* end = base + cut[t + 1];
     while (q < end && li < nlines) {
       const char* r = (const char*)memchr(q, '\n', (size_t)(base + n - q));
       const char* le = r ? r : base + n;
-      if (!parse_line(q, le, width, out + (size_t)li * width)) {
+      if (li >= line0 && !parse_line(q, le, width, out + (size_t)(li - line0) * width)) {
         bad[t] = 1;
         return;
       }
@@ -592,7 +599,8 @@ long long vame_log_append(const char* prefix, int pred, int width, int height, i
   const int nchunks = (nCtus + chunk - 1) / chunk;
   const int ntasks = ng * nchunks;
   std::vector<Buf> out(ntasks);
-  shared_pool(nthreads).run(ntasks, [&](int i) {
+  // threads of this call only: the entry point stays reentrant and fork-safe
+  parallel_for(pick_threads(nthreads, ntasks), ntasks, [&](int i, int) {
     const int g = i / nchunks, c = i % nchunks;
     format_rows(out[i], align, g, c * chunk, std::min(nCtus, (c + 1) * chunk), ctuCols, poc, ref,
                 cost, cpmvs);

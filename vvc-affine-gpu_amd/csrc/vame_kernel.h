@@ -92,8 +92,10 @@ struct KParams {
   PairArgs pair[kMaxPairs];
   const vame_cpmvs_dev* prev[2];  // [align]: 3-CP seeds when the 2-CP pass is not run
   const Item* items;
+  const int32_t* order;      // [nChunks][cpp]: CTU of each padded combination slot, -1 = padding
   int nItems, nCtus, nPairs;
-  int groupPairs, groupPer;  // pair groups of the block order (see affine_me_body)
+  int groupPairs, groupPer;  // groups of the block order (see affine_me_body)
+  int nChunks, cpp;          // CTU chunks per pair, padded combination slots per (pair, chunk)
   int W, H, ctusPerRow;
   int extra;
   int run2, run3;
@@ -1275,23 +1277,27 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   PH_DECL
   PC_DECL
 
-  // ---- XCD-aware block -> (pair group, item, ctu, pair).  The launch's pairs
-  // are taken in groups of groupPairs (about 400 (ctu, pair) combinations, a
-  // working set the XCDs' L2s hold); within a group the order is item-major:
-  // all (ctu, pair) blocks of template item 0 first, then item 1, ...; the
-  // host lists the costlier items first, so the tail is made of short
-  // workgroups.  The host pads a group's combinations to a multiple of 8
-  // (groupPer), so combination j runs on XCD j % 8 (blocks are dealt
-  // round-robin over the 8 XCDs) for every item: the items of one CTU re-read
-  // its reference tile and original samples from the same L2.
+  // ---- XCD-aware block -> (group, item, ctu, pair).  A group is groupPairs
+  // pairs x one chunk of CTU rows (a working set of a few hundred (ctu, pair)
+  // combinations that the XCDs' L2s hold: at 1080p three whole pairs, at 2160p
+  // part of one); within a group the order is item-major: all (ctu, pair)
+  // blocks of template item 0 first, then item 1, ...; the host lists the
+  // costlier items first, so the tail is made of short workgroups.  Each
+  // (pair, chunk) has cpp combination slots, a multiple of 8, so slot j runs
+  // on XCD j % 8 (blocks are dealt round-robin over the 8 XCDs) for every item
+  // and pair: the items of one CTU re-read its reference tile and original
+  // samples from the same L2, and the host's slot -> CTU table (`order`) gives
+  // each XCD a compact strip of CTUs, so neighbouring tiles' margins come from
+  // that L2 too.  Padding slots exit at once.
   const int b = blockIdx.x;
   const int gsz = p.nItems * p.groupPer;
   const int grp = b / gsz, gr = b % gsz;
   const int itemIdx = gr / p.groupPer;
   const int rest = gr % p.groupPer;
-  const int pairIdx = grp * p.groupPairs + rest / p.nCtus;  // (POC, refIdx) pair of this launch
-  if (rest >= p.nCtus * p.groupPairs || pairIdx >= p.nPairs) return;  // padding (uniform, before any barrier)
-  const int ctu = rest % p.nCtus;
+  const int pairIdx = (grp / p.nChunks) * p.groupPairs + rest / p.cpp;  // (POC, refIdx) pair of this launch
+  if (pairIdx >= p.nPairs) return;  // padding (uniform, before any barrier)
+  const int ctu = p.order[(grp % p.nChunks) * p.cpp + rest % p.cpp];
+  if (ctu < 0) return;
   const PairArgs& pa = p.pair[pairIdx];
   const Item* it = p.items + itemIdx;
   const uint16_t* __restrict__ ref = pa.ref;

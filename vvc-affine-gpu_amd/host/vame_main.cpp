@@ -680,6 +680,14 @@ int main(int argc, char** argv) {
   for (int p = 1; p <= N; p++) jobs[((p - 1) / kBatchPocs) % ngpu].pocs.push_back(p);
   print_timestamp("FINISH ALLOCATE MEMORY");
 
+  // the log writer (main.cpp:954-958 -> main_aux_functions.h:387-525) exists
+  // before any worker starts, so a failure here returns with no thread running
+  vame_log_writer* logw = prefix.empty() ? nullptr : vame_log_writer_create(prefix.c_str(), W, H, nthreads);
+  if (!prefix.empty() && !logw) {
+    printf("  [!] ERROR: cannot create the log writer for %s_*\n", prefix.c_str());
+    return 1;
+  }
+
   print_timestamp("START GPU KERNEL");
   const double t0 = now_s();
   std::vector<std::thread> workers;
@@ -704,11 +712,6 @@ int main(int argc, char** argv) {
 
   // ---- writer: POCs in order (main.cpp:954-958 -> main_aux_functions.h:387-525),
   // a whole POC per vame_log_writer_poc call (persistent pool, files kept open)
-  vame_log_writer* logw = prefix.empty() ? nullptr : vame_log_writer_create(prefix.c_str(), W, H, nthreads);
-  if (!prefix.empty() && !logw) {
-    printf("  [!] ERROR: cannot create the log writer for %s_*\n", prefix.c_str());
-    return 1;
-  }
   float pred_ns[4] = {0, 0, 0, 0}, fused_ns = 0;
   long long log_bytes = 0;
   double log_s = 0;

@@ -16,6 +16,7 @@ EXPORTS = (
     "vame_get_timing", "vame_read_frames", "vame_log_remove_old", "vame_log_write_headers",
     "vame_log_append", "vame_log_file_count", "vame_set_prof", "vame_affine_me_batch",
     "vame_log_writer_create", "vame_log_writer_poc", "vame_log_writer_destroy", "vame_pred_mask",
+    "vame_log_writer_refs", "vame_read_frames_range",
 )
 
 
@@ -67,6 +68,7 @@ def lib():
                                       ctypes.POINTER(ctypes.c_int), I]
         C = ctypes.c_char_p
         L.vame_read_frames.argtypes = [C, I, I, I, P, I]
+        L.vame_read_frames_range.argtypes = [C, I, I, I, I, P, I]
         L.vame_log_remove_old.argtypes = [C]
         L.vame_log_write_headers.argtypes = [C, I]
         L.vame_log_append.argtypes = [C, I, I, I, I, I, P, P, I]
@@ -76,6 +78,8 @@ def lib():
         L.vame_log_writer_create.restype = P
         L.vame_log_writer_poc.argtypes = [P, I, I, I, P, P]
         L.vame_log_writer_poc.restype = ctypes.c_longlong
+        L.vame_log_writer_refs.argtypes = [P, I, I, I, I, P, P]
+        L.vame_log_writer_refs.restype = ctypes.c_longlong
         L.vame_log_writer_destroy.argtypes = [P]
         _lib = L
     return _lib

@@ -1,0 +1,355 @@
+"""Frame-sharded end-to-end run over N GPUs, one process per GPU (BASELINE
+configs[4]): the reference's ./main contract -- CSV frames in,
+the 40 per-CU decision-log CSVs out (main.cpp:293-330, :578-1003;
+main_aux_functions.h:387-525) -- with the POC loop cut into contiguous
+(POC, refIdx) pair blocks, one per rank (`shard.pair_shard`).
+
+    python -m vame.distrun -f 240 -s 3840x2160 -q 32 -o orig.csv -r recon.csv \\
+        -l logs/out [--gpus N] [--shard-logs] [--modes all|2cp] [--ExtraGradientIter E]
+
+Every rank reads only the frames its block uses (`vame_read_frames_range`),
+codes its block in launches of up to 32 pairs (`vame_affine_me_batch`), and
+copies each launch's results to pinned host memory while the GPU runs the
+next one.  The logs are written in the reference's order by one of two paths:
+
+  default       the decision-log gather of the north star: rank 0 formats its
+                own block as it completes; every other rank packs its records
+                compactly on its GPU (`shard.pack`), and after the last launch
+                one gather (RCCL over xGMI) brings them to rank 0, which writes
+                them POC by POC.  Rank 0's CPU formats the whole log.
+  --shard-logs  every rank formats its own block (rank 0 into the final files,
+                rank k into part files `<prefix>.partK_*`) as it completes; at
+                the end the ranks exchange the part sizes and copy their parts
+                into the final files at their offsets in parallel
+                (copy_file_range), so formatting scales with the ranks.
+
+Blocks are contiguous in coding order, and a POC cut between two ranks is cut
+at a refIdx boundary (refIdx is the outer loop of every file's rows), so both
+paths give files byte-identical to a one-process run (tests/test_distrun.py).
+Without a launcher, `--gpus N` starts the N ranks itself (vame.launch).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import queue
+import sys
+import threading
+import time
+
+import numpy as np
+import torch
+
+from . import logs, shard
+from .engine import pred_mask
+from .hostlogic import lambda_for_poc, ref_list
+
+RESOLUTIONS = ((3840, 2160), (1920, 1080), (1280, 720), (832, 480), (416, 240))  # constants.h:73-79
+MAX_PAIRS = 32  # pairs per launch (vame_affine_me_batch)
+
+
+def parse_args(argv=None) -> argparse.Namespace:
+    """The reference's options (main.cpp:58-69) plus the frame-shard ones."""
+    ap = argparse.ArgumentParser(prog="vame.distrun")
+    ap.add_argument("-f", "--FramesToBeEncoded", dest="frames", type=int, required=True)
+    ap.add_argument("-s", "--Resolution", dest="res", required=True)
+    ap.add_argument("-q", "--QP", dest="qp", type=int, required=True)
+    ap.add_argument("-o", "--OriginalFrames", dest="orig", required=True)
+    ap.add_argument("-r", "--ReferenceFrames", dest="recon", required=True)
+    ap.add_argument("-l", "--CpmvLogFile", dest="log", default="")
+    ap.add_argument("--ExtraGradientIter", dest="extra", type=int, default=0)
+    ap.add_argument("--modes", choices=("all", "2cp"), default="all")
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--shard-logs", action="store_true")
+    a = ap.parse_args(argv)
+    try:
+        a.W, a.H = (int(v) for v in a.res.lower().split("x"))
+    except ValueError:
+        ap.error(f"bad resolution {a.res!r}")
+    if (a.W, a.H) not in RESOLUTIONS:
+        ap.error(f"unsupported resolution {a.W}x{a.H}")
+    if a.frames < 1 or a.gpus < 1 or not 0 <= a.extra <= 64:
+        ap.error("frames and gpus must be >= 1, ExtraGradientIter in 0..64")
+    a.mode_mask = 3 if a.modes == "all" else 1
+    return a
+
+
+def part_prefix(prefix: str, rank: int) -> str:
+    return f"{prefix}.part{rank}"
+
+
+def launch_batches(blocks):
+    """The block's entries in launches of at most MAX_PAIRS pairs (entries whole)."""
+    out, cur, n = [], [], 0
+    for poc, refs in blocks:
+        if cur and n + len(refs) > MAX_PAIRS:
+            out.append(cur)
+            cur, n = [], 0
+        cur.append((poc, refs))
+        n += len(refs)
+    if cur:
+        out.append(cur)
+    return out
+
+
+class _HostSlots:
+    """Pinned host copies of the results of a launch, one set per slot
+    (reused when the writer has finished with it)."""
+
+    def __init__(self, n_slots: int, pin: bool):
+        self.free = queue.Queue()
+        self.bufs = [dict() for _ in range(n_slots)]
+        self.pin = pin
+        for s in range(n_slots):
+            self.free.put(s)
+
+    def host_like(self, slot: int, key, t: torch.Tensor) -> torch.Tensor:
+        b = self.bufs[slot].get(key)
+        if b is None or b.shape != t.shape:
+            b = torch.empty(t.shape, dtype=t.dtype, pin_memory=self.pin)
+            self.bufs[slot][key] = b
+        return b
+
+
+def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
+    """One rank's whole run; returns its timings.  `engine` needs n_cus,
+    alloc_poc and affine_me_batch (vame.engine.Engine on the GPU; the tests
+    pass an oracle-backed stand-in on CPU ranks)."""
+    t_start = time.perf_counter()
+    W, H, modes = a.W, a.H, a.mode_mask
+    n_cus = (engine.n_cus(0), engine.n_cus(1))
+    cuda = device.type == "cuda"
+    blocks = shard.pair_shard(a.frames, world, rank)
+    T = {"rank": rank, "pairs": sum(len(r) for _, r in blocks), "pocs": len(blocks),
+         "read_csv_s": 0.0, "kernel_s": 0.0, "log_write_s": 0.0, "log_bytes": 0, "gather_s": 0.0,
+         "merge_s": 0.0}
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    # ---- frame ingest: only the frames this block reads (main.cpp:293-330)
+    t = time.perf_counter()
+    d_orig, d_recon = {}, {}
+    if blocks:
+        pocs = [p for p, _ in blocks]
+        need = sorted({ref_list(p)[r] for p, refs in blocks for r in refs})
+        orig = logs.read_frames(a.orig, W, H, pocs[-1] - pocs[0] + 1, first=pocs[0] - 1)
+        recon = logs.read_frames(a.recon, W, H, need[-1] - need[0] + 1, first=need[0])
+        T["read_csv_s"] = time.perf_counter() - t
+        up = lambda f: torch.from_numpy(np.ascontiguousarray(f).view(np.int16)).to(device)  # noqa: E731
+        d_orig = {p: up(orig[p - pocs[0]]) for p in pocs}
+        d_recon = {q: up(recon[q - need[0]]) for q in need}
+        del orig, recon
+
+    # ---- who writes what
+    writes_own = bool(a.log) and (rank == 0 or a.shard_logs)
+    prefix = a.log if rank == 0 else part_prefix(a.log, rank)
+    if a.log and rank == 0:
+        logs.remove_old(a.log)  # removeOldTraces (main.cpp:469)
+    if writes_own and rank > 0:
+        for name in logs.log_names(prefix):
+            if os.path.exists(name):
+                os.remove(name)
+    writer = logs.LogWriter(prefix, W, H) if writes_own else None
+    slab_parts = []
+
+    # ---- the writer thread: formats each launch's POCs once its copy landed
+    slots = _HostSlots(2, cuda)
+    work: queue.Queue = queue.Queue()
+    err = []
+
+    def writer_loop():
+        try:
+            while True:
+                item = work.get()
+                if item is None:
+                    return
+                ev, slot, batch, host = item
+                if ev is not None:
+                    ev.synchronize()
+                t0 = time.perf_counter()
+                for (poc, refs), res in zip(batch, host):
+                    results = {(refs[j], name): (c.numpy(), p.numpy()) for (j, name), (c, p) in res.items()}
+                    T["log_bytes"] += logs.write_poc(prefix, W, H, poc, results, writer=writer)
+                T["log_write_s"] += time.perf_counter() - t0
+                slots.free.put(slot)
+        except Exception as e:  # surfaced after the join
+            err.append(e)
+            slots.free.put(-1)
+
+    th = threading.Thread(target=writer_loop, daemon=True)
+    th.start()
+
+    # ---- the hot path: this block's launches
+    spans = []
+    for batch in launch_batches(blocks):
+        jobs = []
+        for poc, refs in batch:
+            rl = ref_list(poc)
+            jobs.append((d_orig[poc], [d_recon[rl[r]] for r in refs], lambda_for_poc(a.qp, poc),
+                         engine.alloc_poc(len(refs), modes)))
+        if cuda:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        engine.affine_me_batch(jobs, modes, a.extra)
+        if cuda:
+            e1.record()
+            spans.append((e0, e1))
+        if writes_own:
+            slot = slots.free.get()
+            if slot < 0:
+                break
+            host = []
+            for i, job in enumerate(jobs):
+                h = {}
+                for key, (c, p) in job[3].items():
+                    hc = slots.host_like(slot, (i, key, 0), c)
+                    hp = slots.host_like(slot, (i, key, 1), p)
+                    hc.copy_(c, non_blocking=cuda)
+                    hp.copy_(p, non_blocking=cuda)
+                    h[key] = (hc, hp)
+                host.append(h)
+            ev = None
+            if cuda:
+                ev = torch.cuda.Event()
+                ev.record()
+            work.put((ev, slot, batch, host))
+        elif a.log:  # gather path: compact records stay on this GPU until the gather
+            slab_parts.append(shard.pack([j[3] for j in jobs], None, device, modes=modes))
+    work.put(None)
+    th.join()
+    if err:
+        raise err[0]
+    if cuda:
+        torch.cuda.synchronize()
+        T["kernel_s"] = sum(x.elapsed_time(y) for x, y in spans) * 1e-3
+
+    # ---- the decision-log gather into rank 0 (default path)
+    if world > 1 and a.log and not a.shard_logs:
+        t = time.perf_counter()
+        words = max(shard.slab_words(shard.block_layout(shard.pair_shard(a.frames, world, r), modes, n_cus))
+                    for r in range(world))
+        mine = torch.cat(slab_parts) if slab_parts else torch.empty(0, dtype=torch.int32, device=device)
+        slab = torch.cat([mine, mine.new_zeros(words - mine.numel())])
+        if dist.get_backend() == "gloo":
+            slab = slab.cpu()
+        slabs = shard.gather_to_root(slab, world, 0)
+        if cuda:
+            torch.cuda.synchronize()
+        T["gather_s"] = time.perf_counter() - t
+        if rank == 0:
+            t0 = time.perf_counter()
+            for r in range(1, world):
+                o = 0
+                for poc, refs in shard.pair_shard(a.frames, world, r):
+                    w = shard.poc_words(len(refs), modes, n_cus)
+                    res = shard.unpack(slabs[r][o:o + w], [(len(refs), modes, n_cus)])[0]
+                    o += w
+                    results = {(refs[j], name): (c.cpu().numpy(), p.cpu().numpy())
+                               for (j, name), (c, p) in res.items()}
+                    T["log_bytes"] += logs.write_poc(prefix, W, H, poc, results, writer=writer)
+            T["log_write_s"] += time.perf_counter() - t0
+        del slabs
+    if writer is not None:
+        writer.close()
+
+    # ---- --shard-logs: the parts into the final files, every rank in parallel
+    if world > 1 and a.log and a.shard_logs:
+        barrier()
+        t = time.perf_counter()
+        names = logs.log_names(a.log, pred_mask(modes))
+        size = lambda p: os.path.getsize(p) if os.path.exists(p) else 0  # noqa: E731
+        base = {n: size(n) for n in names}
+        parts = {n: [size(part_prefix(a.log, r) + n[len(a.log):]) for r in range(1, world)] for n in names}
+        barrier()  # every rank has read rank 0's sizes before rank 0 grows the files
+        if rank == 0:
+            for n in names:
+                if base[n] or any(parts[n]):
+                    with open(n, "ab") as f:
+                        f.truncate(base[n] + sum(parts[n]))
+        barrier()
+        if rank > 0:
+            for n in names:
+                src = part_prefix(a.log, rank) + n[len(a.log):]
+                if parts[n][rank - 1]:
+                    _copy_into(src, n, base[n] + sum(parts[n][:rank - 1]))
+                if os.path.exists(src):
+                    os.remove(src)
+        barrier()
+        T["merge_s"] = time.perf_counter() - t
+    T["overall_s"] = time.perf_counter() - t_start
+    return T
+
+
+def _copy_into(src: str, dst: str, offset: int) -> None:
+    """All of `src` into `dst` at `offset` (in-kernel copy; plain reads and
+    positioned writes where the file system refuses copy_file_range)."""
+    with open(src, "rb") as s, open(dst, "r+b") as d:
+        n = os.fstat(s.fileno()).st_size
+        done = 0
+        try:
+            while done < n:
+                k = os.copy_file_range(s.fileno(), d.fileno(), n - done, done, offset + done)
+                if k <= 0:
+                    raise OSError("copy_file_range made no progress")
+                done += k
+        except OSError:
+            while done < n:
+                chunk = os.pread(s.fileno(), min(64 << 20, n - done), done)
+                os.pwrite(d.fileno(), chunk, offset + done)
+                done += len(chunk)
+
+
+def report(a, per_rank: list[dict]) -> str:
+    """The reference's timing block (main_aux_functions.h:1416-1446) over the
+    whole job: wall-clock figures are the max over ranks, kernel time summed."""
+    mx = lambda k: max(t[k] for t in per_rank)  # noqa: E731
+    lines = ["=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=", "TIMING RESULTS (nanoseconds)",
+             f"TOTAL_EXEC_TIME({a.frames}x),{sum(t['kernel_s'] for t in per_rank) * 1e9:f}",
+             f"MAX_RANK_EXEC_TIME,{mx('kernel_s') * 1e9:f}",
+             f"OVERALL({a.frames}x),{mx('overall_s'):f}",
+             f"READ_CSV_TIME,{mx('read_csv_s') * 1e9:f}",
+             f"LOG_WRITE_TIME,{mx('log_write_s') * 1e9:f}",
+             f"LOG_GATHER_TIME,{mx('gather_s') * 1e9:f}",
+             f"LOG_MERGE_TIME,{mx('merge_s') * 1e9:f}",
+             f"LOG_BYTES,{sum(t['log_bytes'] for t in per_rank)}",
+             "=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=",
+             "DISTRUN " + json.dumps({"ranks": len(per_rank), "shard_logs": a.shard_logs,
+                                      "per_rank": per_rank})]
+    return "\n".join(lines)
+
+
+def main(argv=None) -> int:
+    a = parse_args(argv)
+    from .launch import init_rank, launch_ranks
+    backend = os.environ.get("VAME_DIST_BACKEND", "nccl")
+    if "WORLD_SIZE" not in os.environ:
+        if a.gpus > 1:  # no launcher: start the ranks (nothing has touched the GPU yet)
+            return launch_ranks(a.gpus, ["-m", "vame.distrun"] + (sys.argv[1:] if argv is None else argv),
+                                backend, "vame.distrun")
+    elif int(os.environ["WORLD_SIZE"]) != a.gpus:
+        print(f"vame.distrun: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {a.gpus}", file=sys.stderr)
+        return 2
+    dist, rank, dev = init_rank(a.gpus, backend)
+    from .engine import Engine
+    eng = Engine(a.W, a.H, dev.index)
+    try:
+        T = run_rank(a, a.gpus, rank, eng, dev, dist)
+    finally:
+        eng.close()
+    per_rank = [T]
+    if dist is not None:
+        per_rank = [None] * a.gpus
+        dist.all_gather_object(per_rank, T)
+    if rank == 0:
+        print(report(a, per_rank), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

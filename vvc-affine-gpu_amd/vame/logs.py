@@ -15,14 +15,36 @@ CPMVS_DTYPE = np.dtype([("nCPs", "<i4"), ("LTx", "<i4"), ("LTy", "<i4"), ("RTx",
                         ("RTy", "<i4"), ("LBx", "<i4"), ("LBy", "<i4")])
 
 
-def read_frames(path: str, width: int, height: int, n_frames: int, nthreads: int = 0) -> np.ndarray:
-    """(n_frames, H, W) uint16 from a reference-layout CSV (or raw .u16/.yuv)."""
+def read_frames(path: str, width: int, height: int, n_frames: int, nthreads: int = 0,
+                first: int = 0) -> np.ndarray:
+    """(n_frames, H, W) uint16 from a reference-layout CSV (or raw .u16/.yuv):
+    frames first .. first + n_frames - 1 of the file."""
     out = np.empty((n_frames, height, width), np.uint16)
-    rc = lib().vame_read_frames(path.encode(), width, height, n_frames,
-                                out.ctypes.data_as(ctypes.c_void_p), nthreads)
+    rc = lib().vame_read_frames_range(path.encode(), width, height, first, n_frames,
+                                      out.ctypes.data_as(ctypes.c_void_p), nthreads)
     if rc != 0:
-        raise VameError(f"cannot read {n_frames} frames of {width}x{height} from {path} (rc={rc})")
+        raise VameError(f"cannot read frames {first}..{first + n_frames - 1} of {width}x{height} "
+                        f"from {path} (rc={rc})")
     return out
+
+
+def log_names(prefix: str, pred_mask: int = 15) -> list[str]:
+    """The distinct decision-log files of the PREDs in pred_mask, in PRED and
+    group order (main_aux_functions.h:392-425: HALF groups of one W x H share a file)."""
+    names = []
+    L = lib()
+    w, h, n, st = (ctypes.c_int() for _ in range(4))
+    xs, ys = (ctypes.c_int * 64)(), (ctypes.c_int * 64)()
+    for m, tag in enumerate(PREDS):
+        if not (pred_mask >> m) & 1:
+            continue
+        for g in range(L.vame_num_groups(m >> 1)):
+            L.vame_group_geometry(m >> 1, g, ctypes.byref(w), ctypes.byref(h), ctypes.byref(n),
+                                  ctypes.byref(st), xs, ys)
+            name = f"{prefix}_{tag[:4]}_{tag[5]}CPs_{w.value}x{h.value}.csv"
+            if name not in names:
+                names.append(name)
+    return names
 
 
 def remove_old(prefix: str) -> None:
@@ -69,11 +91,13 @@ class LogWriter:
             raise VameError(f"cannot create a log writer for {prefix} ({width}x{height})")
 
     def poc(self, poc: int, results) -> int:
-        """results: {(ref, PRED name): (cost, cpmvs)}; refs 0..n-1, each with
-        the same PREDs."""
+        """results: {(ref, PRED name): (cost, cpmvs)}; refs r0..r0+n-1 (r0 = 0
+        unless the POC is cut between frame-shard ranks), each with the same
+        PREDs."""
         refs = sorted({r for r, _ in results})
-        if refs != list(range(len(refs))):
-            raise ValueError("refIdx must run 0..n-1")
+        if not refs or refs != list(range(refs[0], refs[0] + len(refs))) or refs[-1] > 3:
+            raise ValueError("refIdx must be a contiguous range within 0..3")
+        r0 = refs[0]
         mask = 0
         for m, name in enumerate(PREDS):
             if any((r, name) in results for r in refs):
@@ -89,9 +113,9 @@ class LogWriter:
                     raise ValueError(f"refIdx {r} lacks {name}")
                 c, p = _arrays(m, self.width, self.height, *results[(r, name)])
                 keep += [c, p]
-                cost_p[r * 4 + m] = c.ctypes.data
-                cp_p[r * 4 + m] = p.ctypes.data
-        nb = lib().vame_log_writer_poc(self._w, poc, len(refs), mask, cost_p, cp_p)
+                cost_p[(r - r0) * 4 + m] = c.ctypes.data
+                cp_p[(r - r0) * 4 + m] = p.ctypes.data
+        nb = lib().vame_log_writer_refs(self._w, poc, r0, len(refs), mask, cost_p, cp_p)
         if nb < 0:
             raise VameError("writing the log files failed")
         return nb

@@ -71,7 +71,7 @@ class ShardRun:
             self.eng.affine_me_batch(self.jobs, self.modes, 0)
 
     def slab(self) -> torch.Tensor:
-        return shard.pack([j[3] for j in self.jobs], self.words, self.device)
+        return shard.pack([j[3] for j in self.jobs], self.words, self.device, modes=self.modes)
 
     def gather(self):
         """The decision-record gather into rank 0: (slabs on rank 0 / None, bytes
@@ -84,27 +84,39 @@ class ShardRun:
         slabs = shard.gather_to_root(slab, self.world, 0)
         return slabs, 4 * self.words * (self.world - 1)
 
-    def verify(self, slabs, per_rank: int = 2):
-        """Rank 0: recompute up to `per_rank` block entries of every rank (its
-        first and last POC, with that rank's refs; a single-rank run recomputes
-        its own) and compare their records with the gathered slab, word for
-        word."""
+    def cut_pocs(self) -> list[int]:
+        """POCs whose refIdx range is split between two ranks' pair blocks."""
+        owners: dict[int, set] = {}
+        for r in range(self.world):
+            for poc, _ in shard.pair_shard(self.n, self.world, r, self.n_pairs):
+                owners.setdefault(poc, set()).add(r)
+        return sorted(p for p, o in owners.items() if len(o) > 1)
+
+    def verify(self, slabs, full: bool = False):
+        """Rank 0: recompute block entries of every rank -- its first and last
+        POC (with that rank's refs), both halves of every POC cut between two
+        ranks, or with `full` every entry -- and compare their records with the
+        gathered slab, word for word."""
         checked, ok = [], True
+        cuts = set(self.cut_pocs())
         for r in range(self.world):
             blocks = shard.pair_shard(self.n, self.world, r, self.n_pairs)
             if not blocks:
                 continue
-            idx = sorted({0, len(blocks) - 1})[:per_rank]
+            idx = sorted(set(range(len(blocks))) if full else
+                         {0, len(blocks) - 1} | {i for i, (poc, _) in enumerate(blocks) if poc in cuts})
             offs, o = [], 0
             for _, refs in blocks:
                 offs.append(o)
                 o += shard.poc_words(len(refs), self.modes, self.n_cus)
-            sample = [blocks[i] for i in idx]
-            jobs = self._jobs(sample)
-            self.eng.affine_me_batch(jobs, self.modes, 0)
-            for i, (poc, refs), job in zip(idx, sample, jobs):
-                want = shard.pack([job[3]], None, self.device)
-                got = slabs[r][offs[i]:offs[i] + want.numel()]
-                ok &= bool(torch.equal(got.to(want.device), want))
-                checked.append([poc, refs])
-        return {"pocs": checked, "byte_identical": ok}
+            for k in range(0, len(idx), 8):  # recompute in batches of 8 block entries
+                part = idx[k:k + 8]
+                sample = [blocks[i] for i in part]
+                jobs = self._jobs(sample)
+                self.eng.affine_me_batch(jobs, self.modes, 0)
+                for i, (poc, refs), job in zip(part, sample, jobs):
+                    want = shard.pack([job[3]], None, self.device, modes=self.modes)
+                    got = slabs[r][offs[i]:offs[i] + want.numel()]
+                    ok &= bool(torch.equal(got.to(want.device), want))
+                    checked.append([poc, refs, r])
+        return {"pocs": checked, "cut_pocs": sorted(cuts), "byte_identical": ok}

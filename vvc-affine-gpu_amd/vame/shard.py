@@ -103,26 +103,29 @@ def merge_blocks(block_lists, results_lists) -> dict[int, dict]:
 
 
 def result_keys(nrefs: int, modes: int):
-    """(refIdx, MODE) keys of one POC's results, in the fixed wire order."""
-    keys = []
-    for r in range(nrefs):
-        for m, name in enumerate(MODES):
-            if (m & 1) and not (modes & 2):
-                continue
-            keys.append((r, name))
-    return keys
+    """(refIdx, MODE) keys of one POC's results, in the fixed wire order: the
+    PREDs the mode mask codes (engine.pred_mask: 2-CP / 3-CP and the
+    FULL / HALF selection), refIdx outer."""
+    from .engine import pred_mask
+    preds = pred_mask(modes)
+    return [(r, name) for r in range(nrefs) for m, name in enumerate(MODES) if (preds >> m) & 1]
 
 
 def ncp_of(mode: str) -> int:
     return 3 if mode.endswith("3CP") else 2
 
 
-def pack(results: list[dict], words: int | None = None, device=None) -> torch.Tensor:
+def pack(results: list[dict], words: int | None = None, device=None, modes: int | None = None) -> torch.Tensor:
     """Concatenate the results of several POCs ({(ref, MODE): (cost int64[n],
     cpmv int32[n, 7])}, in POC order) into one int32 slab of compact records,
-    zero padded to `words`."""
+    zero padded to `words`.  With `modes`, every POC must hold exactly the
+    keys `unpack` will expect for that mode mask."""
     parts = []
     for res in results:
+        if modes is not None:
+            nrefs = max(r for r, _ in res) + 1 if res else 0
+            if sorted(res, key=lambda k: (k[0], MODES.index(k[1]))) != result_keys(nrefs, modes):
+                raise ValueError(f"results {sorted(res)} do not match mode mask {modes}")
         for key in sorted(res, key=lambda k: (k[0], MODES.index(k[1]))):
             cost, cpmv = res[key]
             parts.append(cost.reshape(-1).to(torch.int32))
@@ -170,15 +173,15 @@ def poc_words(nrefs: int, modes: int, n_cus_per_align: tuple[int, int]) -> int:
 
 def gather_to_root(slab: torch.Tensor, world: int, root: int = 0, group=None):
     """The one exchange step: every rank's equal-size slab to
-    `root` only (RCCL over xGMI on the GPU box: one ring-free gather into the
+    `root` (a rank of `group`, default the whole world) only (RCCL over xGMI on the GPU box: one ring-free gather into the
     root, 1/world of an all_gather's traffic).  Returns the list of slabs on
     the root, None elsewhere."""
     import torch.distributed as dist
     if world == 1:
         return [slab]
-    rank = dist.get_rank(group)
+    rank = dist.get_rank(group)  # rank within the group; dist.gather's dst is a global rank
     dst = [torch.empty_like(slab) for _ in range(world)] if rank == root else None
-    dist.gather(slab, dst, dst=root, group=group)
+    dist.gather(slab, dst, dst=root if group is None else dist.get_global_rank(group, root), group=group)
     return dst
 
 
