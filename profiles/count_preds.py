@@ -41,7 +41,7 @@ def main():
     dev = torch.device("cuda", 0)
     eng = Engine(cfg["W"], cfg["H"], 0)
     run = ShardRun(eng, cfg["W"], cfg["H"], qp, cfg["frames"], cfg["modes"], 1, 0, dev)
-    cnt = (ctypes.c_ulonglong * 2)()
+    cnt = (ctypes.c_ulonglong * 4)()
     L.vame_debug_pred_count(cnt, 1)
     run.step()
     torch.cuda.synchronize()
@@ -51,7 +51,9 @@ def main():
     out = {"config": args.config, "qp": qp, "pairs": run.pairs,
            "executed_quad": cnt[0], "algorithmic_quad": alg_q, "executed_pred_frac_quad": cnt[0] / alg_q,
            "executed_ctu": cnt[1], "algorithmic_ctu": alg_b, "executed_pred_frac_ctu": cnt[1] / alg_b,
-           "executed_pred_frac": (cnt[0] + cnt[1]) / (alg_q + alg_b)}
+           "executed_pred_frac": (cnt[0] + cnt[1]) / (alg_q + alg_b),
+           # executed predictions whose 9x9 window left the staged tile (clamped global loads)
+           "outside_tile_frac_quad": cnt[2] / max(cnt[0], 1), "outside_tile_frac_ctu": cnt[3] / max(cnt[1], 1)}
     print(json.dumps(out))
     eng.close()
 

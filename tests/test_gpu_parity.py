@@ -354,3 +354,26 @@ def test_property_translation_1080p(engines, d):
         cp[f] = p[:, i]
     frac, n = translation_ok_fraction(cp, W, H, d)
     assert n > 1000 and frac >= 0.75, (frac, n)
+
+
+@pytest.mark.parametrize("combos,order", [(16, 0), (24, 1), (64, 2), (408, 4), (100, 3)])
+def test_block_order_variants(combos, order, monkeypatch):
+    """The block order's knobs (VAME_GROUP_COMBOS / _BIG, VAME_XCD_ORDER, read
+    at vame_create: CTU chunks, XCD dealing) only move work between XCDs: a
+    1080p POC with 2 refs gives the default context's results bit for bit."""
+    from vame.engine import Engine
+    from vame import synth
+    o, r = synth.synth_sequence(1920, 1080, 2, 32, seed=0x0DE5)
+    cur, refs = dev(o[1]), [dev(r[1]), dev(r[0])]
+    base = Engine(1920, 1080, 0)
+    want = base.affine_me_poc(cur, refs, 70.335619, modes=3)
+    monkeypatch.setenv("VAME_GROUP_COMBOS", str(combos))
+    monkeypatch.setenv("VAME_GROUP_COMBOS_BIG", str(max(8, combos // 2)))
+    monkeypatch.setenv("VAME_XCD_ORDER", str(order))
+    eng = Engine(1920, 1080, 0)
+    got = eng.affine_me_poc(cur, refs, 70.335619, modes=3)
+    torch.cuda.synchronize()
+    for k in want:
+        assert torch.equal(want[k][0], got[k][0]) and torch.equal(want[k][1], got[k][1]), k
+    eng.close()
+    base.close()

@@ -39,9 +39,10 @@ struct vame_ctx {
   Item* dQuad = nullptr;
   Item* dBig = nullptr;
   int nQuadFull = 0, nQuadHalf = 0, nBig = 0;
-  // block order (block_grid): slot -> CTU table, CTU chunks, slots per (pair, chunk)
-  int32_t* dOrder = nullptr;
-  int groupCombos = 408, nChunks = 1, cpp = 0;
+  // block order (block_grid), per kernel class (0 quadrant, 1 128-class):
+  // slot -> CTU table, group size, CTU chunks, slots per (pair, chunk)
+  int32_t* dOrder[2] = {nullptr, nullptr};
+  int groupCombos[2] = {408, 408}, nChunks[2] = {1, 1}, cpp[2] = {0, 0};
   hipStream_t side = nullptr;   // second stream: 128-class items run beside the quadrant items
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   // optional per-kernel timing: (start, end) event pairs per kernel class
@@ -257,47 +258,57 @@ struct DeviceGuard {
 // combinations of each template item in slots padded to a multiple of 8 per
 // (pair, chunk), so every item of a CTU lands on the same XCD (padding blocks
 // exit at once).  Returns the grid size.
-unsigned block_grid(const vame_ctx* c, KParams& k) {
-  k.order = c->dOrder;
-  k.nChunks = c->nChunks;
-  k.cpp = c->cpp;
-  k.groupPairs = c->nChunks > 1 ? 1 : std::max(1, std::min(k.nPairs, c->groupCombos / c->cpp));
-  k.groupPer = k.groupPairs * c->cpp;
-  const int groups = (k.nPairs + k.groupPairs - 1) / k.groupPairs * c->nChunks;
+unsigned block_grid(const vame_ctx* c, int cls, KParams& k) {
+  k.order = c->dOrder[cls];
+  k.nChunks = c->nChunks[cls];
+  k.cpp = c->cpp[cls];
+  k.groupPairs = k.nChunks > 1 ? 1 : std::max(1, std::min(k.nPairs, c->groupCombos[cls] / k.cpp));
+  k.groupPer = k.groupPairs * k.cpp;
+  const int groups = (k.nPairs + k.groupPairs - 1) / k.groupPairs * k.nChunks;
   return (unsigned)(groups * k.nItems * k.groupPer);
 }
 
 // The slot -> CTU table of the block order: the frame's CTU rows cut into
 // chunks of at most groupCombos CTUs; within a chunk, slot j runs on XCD j % 8
-// (workgroups are dealt round-robin over the XCDs), and with xcdOrder = 1 XCD
-// x takes the x-th eighth of the chunk's CTUs in column-major order -- a
-// compact strip, so the margins of neighbouring reference tiles hit that
-// XCD's L2 -- while xcdOrder = 0 deals the CTUs in raster order.
+// (workgroups are dealt round-robin over the XCDs).  xcdOrder picks which
+// CTUs share an XCD: 0 deals the chunk's CTUs one by one in raster order
+// (neighbours on different XCDs: the per-XCD load follows the frame's content
+// evenly); R >= 2 deals runs of R raster-adjacent CTUs (neighbours share the
+// margins of their reference tiles in one L2); 1 gives XCD x the x-th eighth
+// of the chunk in column-major order (compact strips: fewest fetches, but an
+// XCD's load follows the content of its strip).
 std::vector<int32_t> build_order(int nCtus, int cols, int groupCombos, int xcdOrder, int& nChunks,
                                  int& cpp) {
   const int rows = nCtus / cols;
   nChunks = (nCtus + groupCombos - 1) / groupCombos;
   const int rowsPer = (rows + nChunks - 1) / nChunks;
   nChunks = (rows + rowsPer - 1) / rowsPer;
-  const int seg = (rowsPer * cols + 7) / 8;
-  cpp = seg * 8;
+  const int R = std::max(1, xcdOrder == 1 ? 1 : xcdOrder);
+  const int maxN = rowsPer * cols;
+  const int perXcd = xcdOrder == 1 ? (maxN + 7) / 8 : ((maxN + R - 1) / R + 7) / 8 * R;
+  cpp = perXcd * 8;
   std::vector<int32_t> order((size_t)nChunks * cpp, -1);
   for (int ch = 0; ch < nChunks; ch++) {
     const int r0 = ch * rowsPer, r1 = std::min(rows, r0 + rowsPer);
     std::vector<int> L;
-    if (xcdOrder)
+    if (xcdOrder == 1)
       for (int x = 0; x < cols; x++)
         for (int y = r0; y < r1; y++) L.push_back(y * cols + x);
     else
       for (int y = r0; y < r1; y++)
         for (int x = 0; x < cols; x++) L.push_back(y * cols + x);
+    const int n = (int)L.size();
     int32_t* o = order.data() + (size_t)ch * cpp;
-    if (xcdOrder) {
-      const int s = ((int)L.size() + 7) / 8;  // CTUs per XCD in this chunk
+    if (xcdOrder == 1) {
+      const int s = (n + 7) / 8;  // CTUs per XCD in this chunk
       for (int x = 0; x < 8; x++)
-        for (int i = 0; i < s && x * s + i < (int)L.size(); i++) o[8 * i + x] = L[x * s + i];
-    } else {
-      for (size_t j = 0; j < L.size(); j++) o[j] = L[j];
+        for (int i = 0; i < s && x * s + i < n; i++) o[8 * i + x] = L[x * s + i];
+    } else {  // run k -> XCD k % 8; XCD x's i-th slot = element i % R of its (i / R)-th run
+      for (int x = 0; x < 8; x++)
+        for (int i = 0; i < perXcd; i++) {
+          const int e = (x + 8 * (i / R)) * R + i % R;
+          if (e < n) o[8 * i + x] = L[e];
+        }
     }
   }
   return order;
@@ -346,7 +357,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     KParams kb = kp;
     kb.items = c->dBig;
     kb.nItems = c->nBig;
-    const unsigned grid = block_grid(c, kb);
+    const unsigned grid = block_grid(c, 1, kb);
     VAME_TRY(time_begin(c, 1, sBig));
     hipLaunchKernelGGL(kernel_for<true>(c->prof, mode), dim3(grid),
                        dim3(Cfg<128>::THREADS), 0, sBig, kb);
@@ -358,7 +369,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     KParams kq = kp;
     kq.items = quadFull ? c->dQuad : c->dQuad + c->nQuadFull;
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
-    const unsigned grid = block_grid(c, kq);
+    const unsigned grid = block_grid(c, 0, kq);
     VAME_TRY(time_begin(c, 0, sQuad));
     hipLaunchKernelGGL(kernel_for<false>(c->prof, mode), dim3(grid),
                        dim3(Cfg<64>::THREADS), 0, sQuad, kq);
@@ -435,14 +446,18 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   c->nQuadHalf = (int)qh.size();
   std::vector<Item> quad(qf);
   quad.insert(quad.end(), qh.begin(), qh.end());
-  // tuning knobs of the block order (defaults measured on MI355X, DESIGN.md §4)
-  c->groupCombos = std::max(8, env_int("VAME_GROUP_COMBOS", 408));
-  const std::vector<int32_t> order = build_order(nCtus, c->ctusPerRow, c->groupCombos,
-                                                 env_int("VAME_XCD_ORDER", 1), c->nChunks, c->cpp);
   hipError_t e = hipMalloc(&c->dQuad, quad.size() * sizeof(Item));
-  if (e == hipSuccess) e = hipMalloc(&c->dOrder, order.size() * sizeof(int32_t));
-  if (e == hipSuccess)
-    e = hipMemcpy(c->dOrder, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice);
+  // tuning knobs of the block order (defaults measured on MI355X, DESIGN.md §4)
+  const int xcdOrder = env_int("VAME_XCD_ORDER", 0);
+  c->groupCombos[0] = std::max(8, env_int("VAME_GROUP_COMBOS", 408));
+  c->groupCombos[1] = std::max(8, env_int("VAME_GROUP_COMBOS_BIG", c->groupCombos[0]));
+  for (int k = 0; k < 2 && e == hipSuccess; k++) {
+    const std::vector<int32_t> order =
+        build_order(nCtus, c->ctusPerRow, c->groupCombos[k], xcdOrder, c->nChunks[k], c->cpp[k]);
+    e = hipMalloc(&c->dOrder[k], order.size() * sizeof(int32_t));
+    if (e == hipSuccess)
+      e = hipMemcpy(c->dOrder[k], order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipMalloc(&c->dBig, big.size() * sizeof(Item));
   if (e == hipSuccess) e = hipMemcpy(c->dQuad, quad.data(), quad.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->dBig, big.data(), big.size() * sizeof(Item), hipMemcpyHostToDevice);
@@ -463,7 +478,8 @@ void vame_destroy(vame_ctx* c) {
   DeviceGuard guard(c->device);
   if (c->dQuad) (void)hipFree(c->dQuad);
   if (c->dBig) (void)hipFree(c->dBig);
-  if (c->dOrder) (void)hipFree(c->dOrder);
+  for (int k = 0; k < 2; k++)
+    if (c->dOrder[k]) (void)hipFree(c->dOrder[k]);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->evFork) (void)hipEventDestroy(c->evFork);
   if (c->evJoin) (void)hipEventDestroy(c->evJoin);
@@ -620,13 +636,14 @@ int vame_debug_phase_cycles(unsigned long long* out32, int reset) {
 }
 #endif
 #if VAME_COUNT_PRED
-// instrumentation builds: sub-block predictions run, [quad, ctu] (see vame_kernel.h)
-int vame_debug_pred_count(unsigned long long* out2, int reset) {
-  if (!out2) return VAME_E_INVALID;
+// instrumentation builds: sub-block predictions run, [quad, ctu], and those of
+// them whose window left the staged tile, [2 + quad, 2 + ctu] (see vame_kernel.h)
+int vame_debug_pred_count(unsigned long long* out4, int reset) {
+  if (!out4) return VAME_E_INVALID;
   VAME_HIP(hipDeviceSynchronize());
-  VAME_HIP(hipMemcpyFromSymbol(out2, HIP_SYMBOL(g_pred_count), sizeof(unsigned long long) * 2));
+  VAME_HIP(hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_pred_count), sizeof(unsigned long long) * 4));
   if (reset) {
-    unsigned long long z[2] = {};
+    unsigned long long z[4] = {};
     VAME_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pred_count), z, sizeof(z)));
   }
   return VAME_OK;

@@ -125,12 +125,13 @@ constexpr int kSolvePrio = 3;
 
 // VAME_COUNT_PRED (instrumentation builds, libvame_count.so): every lane counts
 // the sub-block predictions it runs (the exact early exit skips the rest of
-// the algorithmic n_pred per sub-block); g_pred_count[kernel: quad, ctu].
+// the algorithmic n_pred per sub-block); g_pred_count[kernel: quad, ctu], and
+// [2 + kernel]: those whose 9x9 window left the staged tile (clamped-global path).
 #ifndef VAME_COUNT_PRED
 #define VAME_COUNT_PRED 0
 #endif
 #if VAME_COUNT_PRED
-__device__ unsigned long long g_pred_count[2];
+__device__ unsigned long long g_pred_count[4];
 #define PC_DECL unsigned pc_n = 0;
 #define PC_ADD pc_n++;
 #define PC_FLUSH { if (pc_n) atomicAdd(&g_pred_count[REGION == 128], (unsigned long long)pc_n); }
@@ -602,6 +603,13 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   const int wx = g.x + sx + ix - 2, wy = g.y + sy + iy - 2;  // window origin (frame)
   const int tx = wx - tx0, ty = wy - ty0;
   const bool inTile = (unsigned)tx <= (unsigned)(TILE - 9) && (unsigned)ty <= (unsigned)(TILE - 9);
+#if VAME_COUNT_PRED
+  {  // instrumentation: windows outside the tile, one atomic per wave
+    const unsigned long long out = __builtin_amdgcn_ballot_w64(!inTile);
+    if (out && __lane_id() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
+      atomicAdd(&g_pred_count[2 + (TILE > 100)], (unsigned long long)__popcll(out));
+  }
+#endif
   if (!PROF && __builtin_amdgcn_ballot_w64(!(inTile && (fx | fy) == 0)) == 0) {
     // Every active lane has an integer MV inside the tile (e.g. every sub-block
     // of the first 2-CP prediction, from zero CPMVs): the phase-0 filter is the

@@ -62,6 +62,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--modes", choices=("all", "2cp"), default="all")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--shard-logs", action="store_true")
+    ap.add_argument("--rank-only", type=int, default=None, metavar="K",
+                    help="run only rank K's share of a --gpus N job, alone on GPU 0 (no collective; "
+                         "its logs stay part files): prices one rank of an N-GPU node on one GPU")
     a = ap.parse_args(argv)
     try:
         a.W, a.H = (int(v) for v in a.res.lower().split("x"))
@@ -71,6 +74,8 @@ def parse_args(argv=None) -> argparse.Namespace:
         ap.error(f"unsupported resolution {a.W}x{a.H}")
     if a.frames < 1 or a.gpus < 1 or not 0 <= a.extra <= 64:
         ap.error("frames and gpus must be >= 1, ExtraGradientIter in 0..64")
+    if a.rank_only is not None and not 0 <= a.rank_only < a.gpus:
+        ap.error("--rank-only K needs 0 <= K < --gpus")
     a.mode_mask = 3 if a.modes == "all" else 1
     return a
 
@@ -256,7 +261,7 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
         writer.close()
 
     # ---- --shard-logs: the parts into the final files, every rank in parallel
-    if world > 1 and a.log and a.shard_logs:
+    if world > 1 and a.log and a.shard_logs and dist is not None:
         barrier()
         t = time.perf_counter()
         names = logs.log_names(a.log, pred_mask(modes))
@@ -325,6 +330,18 @@ def main(argv=None) -> int:
     a = parse_args(argv)
     from .launch import init_rank, launch_ranks
     backend = os.environ.get("VAME_DIST_BACKEND", "nccl")
+    if a.rank_only is not None:  # one rank of an N-rank job, alone (no process group)
+        from .engine import Engine
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        eng = Engine(a.W, a.H, 0)
+        try:
+            a.shard_logs = True  # its rows stay in its own (part) files
+            T = run_rank(a, a.gpus, a.rank_only, eng, dev)
+        finally:
+            eng.close()
+        print(report(a, [T]), flush=True)
+        return 0
     if "WORLD_SIZE" not in os.environ:
         if a.gpus > 1:  # no launcher: start the ranks (nothing has touched the GPU yet)
             return launch_ranks(a.gpus, ["-m", "vame.distrun"] + (sys.argv[1:] if argv is None else argv),
