@@ -264,7 +264,7 @@ def load_profile(config: str, avg_launch_ms: float) -> dict:
     out = {"traffic": p.get("quad_hbm_bytes_per_launch"),
            "executed_pred_frac": p.get("executed_pred_frac")}
     sq = p.get("quad_sq")
-    if sq:
+    if sq and avg_launch_ms > 0:
         clk = sq["clock_ghz"]
         cycles = avg_launch_ms * 1e-3 * clk * 1e9
         rate = sq["insts_valu_per_launch"] / (N_SIMD * cycles)
