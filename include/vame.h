@@ -142,6 +142,16 @@ int vame_read_frames(const char* path, int width, int height, int nframes, uint1
  * rank reads only the frames its POC block uses). */
 int vame_read_frames_range(const char* path, int width, int height, int first, int nframes,
                            uint16_t* out, int nthreads);
+/* The same, reading only the bytes [span_begin, span_end) of a CSV (span_end < 0:
+ * to the end), which must hold every line of those frames, with lines_before =
+ * the number of '\n' in [0, span_begin) -- so a rank whose frames lie deep in
+ * a large file does not scan the bytes ahead of them.  vame_count_lines counts
+ * the '\n' of [begin, end) (end < 0: to the end; ranks count disjoint chunks
+ * and exchange the counts). */
+long long vame_count_lines(const char* path, long long begin, long long end, int nthreads);
+int vame_read_frames_span(const char* path, int width, int height, int first, int nframes,
+                          long long span_begin, long long lines_before, long long span_end,
+                          uint16_t* out, int nthreads);
 
 /* Decision log (main_aux_functions.h:387-525, 1547-1585).  pred = 0 FULL_2CP,
  * 1 FULL_3CP, 2 HALF_2CP, 3 HALF_3CP (constants.h:15-21).  Files are
@@ -179,6 +189,20 @@ long long vame_log_writer_poc(vame_log_writer* w, int poc, int nrefs, int pred_m
 long long vame_log_writer_refs(vame_log_writer* w, int poc, int ref0, int nrefs, int pred_mask,
                                const int64_t* const* cost, const vame_cpmvs* const* cpmvs);
 int vame_log_writer_destroy(vame_log_writer* w);
+/* Deferred mode, for a frame-shard rank whose rows belong in the middle of
+ * the files: after vame_log_writer_set_deferred(w, 1) the writer keeps each
+ * file's rows in host memory instead of appending them.  Its files are
+ * numbered 0 .. vame_log_writer_num_files - 1 (vame_log_writer_file_name);
+ * vame_log_writer_sizes reports the bytes held per file, and
+ * vame_log_writer_flush_at writes every file's rows at offsets[f] (pwrite;
+ * the file is created if missing and never truncated), files in parallel,
+ * returning the bytes written -- so the ranks of a node, once they know each
+ * other's sizes, place their blocks into the one set of files at once. */
+int vame_log_writer_set_deferred(vame_log_writer* w, int deferred);
+int vame_log_writer_num_files(vame_log_writer* w);
+int vame_log_writer_file_name(vame_log_writer* w, int f, char* buf, int buflen);
+int vame_log_writer_sizes(vame_log_writer* w, long long* sizes);
+long long vame_log_writer_flush_at(vame_log_writer* w, const long long* offsets);
 
 const char* vame_strerror(int code);
 const char* vame_last_hip_error(void);

@@ -13,7 +13,7 @@ O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 B="python3 $R/bench.py --config $CFG"
-P="--no-spans --no-cpu-baseline --steps 10 --warmup 2"
+P="--no-spans --no-cpu-baseline --steps ${PSTEPS:-10} --warmup ${PWARM:-2}"  # c5: PSTEPS=1 PWARM=0
 echo "[prof] bench line"
 timeout -k 10 600 $B "$@" > $O/bench.json 2> $O/bench.err
 cat $O/bench.json

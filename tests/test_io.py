@@ -380,3 +380,67 @@ def test_read_frames_range(tmp_path):
                 assert (logs.read_frames(path, 416, 240, n, t, first=first) == fr[first:first + n]).all()
         with pytest.raises(logs.VameError):
             logs.read_frames(path, 416, 240, 2, first=4)
+
+
+@pytest.mark.parametrize("K", [1, 3, 7, 40])
+def test_read_frames_span_from_chunk_index(tmp_path, K):
+    """vame_count_lines over K byte chunks + line_span + vame_read_frames_span
+    (the frame-shard ranks' ingest): any frame range read through the chunks
+    that hold it equals the slice of a whole read; the bytes ahead of the span
+    are never parsed."""
+    rng = np.random.default_rng(K)
+    fr = rng.integers(0, 1024, size=(6, 240, 416)).astype(np.uint16)
+    p = str(tmp_path / "f.csv")
+    write_csv(p, fr)
+    size = os.path.getsize(p)
+    bounds = [size * k // K for k in range(K + 1)]
+    counts = [logs.count_lines(p, bounds[k], bounds[k + 1], nthreads=3) for k in range(K)]
+    assert sum(counts) == logs.count_lines(p) == 6 * 240
+    prefix = [0] + list(np.cumsum(counts))
+    for first, n in ((0, 6), (0, 1), (2, 3), (5, 1), (3, 2)):
+        span = logs.line_span(bounds, prefix, first * 240, (first + n) * 240)
+        assert span[0] <= size and span[2] <= size
+        got = logs.read_frames(p, 416, 240, n, 4, first=first, span=span)
+        assert (got == fr[first:first + n]).all(), (first, n, span)
+    # a span that misses the frames' last line is refused
+    with pytest.raises(logs.VameError):
+        logs.read_frames(p, 416, 240, 3, first=0, span=(0, 0, size // 3))
+
+
+def test_log_writer_deferred_flush_at(tmp_path):
+    """Deferred writers (vame_log_writer_set_deferred / _sizes / _flush_at):
+    three writers each hold one block of POCs (one block starts inside POC 5,
+    at refIdx 2) and place it into the same files at the byte offsets of the
+    blocks before it; the files equal one writer appending every POC."""
+    rng = np.random.default_rng(12)
+    pocs = {p: _random_poc(rng, 416, 240, range(min(4, p))) for p in range(1, 8)}
+    a = tmp_path / "one"
+    a.mkdir()
+    with logs.LogWriter(str(a / "log"), 416, 240) as w:
+        for p, res in pocs.items():
+            logs.write_poc(str(a / "log"), 416, 240, p, res, writer=w)
+    b = tmp_path / "three"
+    b.mkdir()
+    pre = str(b / "log")
+    cut = {k: v for k, v in pocs[5].items() if k[0] < 2}, {k: v for k, v in pocs[5].items() if k[0] >= 2}
+    blocks = [[(p, pocs[p]) for p in (1, 2, 3)], [(4, pocs[4]), (5, cut[0])], [(5, cut[1]), (6, pocs[6]), (7, pocs[7])]]
+    writers = [logs.LogWriter(pre, 416, 240, nthreads=3) for _ in blocks]
+    for k in (1, 2):
+        writers[k].defer()
+    for w, blk in zip(writers, blocks):
+        for p, res in blk:
+            logs.write_poc(pre, 416, 240, p, res, writer=w)
+    writers[0].close()
+    names = writers[1].files()
+    assert names == logs.log_names(pre)
+    base = [os.path.getsize(n) if os.path.exists(n) else 0 for n in names]
+    s1, s2 = writers[1].held_sizes(), writers[2].held_sizes()
+    # flush the later block first: the files grow with holes, then fill in
+    writers[2].flush_at([x + y for x, y in zip(base, s1)])
+    writers[1].flush_at(base)
+    for w in writers[1:]:
+        w.close()
+    fa = _files(a)
+    assert fa == _files(b) and len(fa) == 40
+    for f in fa:
+        assert (a / f).read_bytes() == (b / f).read_bytes(), f

@@ -352,6 +352,16 @@ struct vame_log_writer {
   std::vector<int> predOf;
   std::vector<int> fds;
   std::vector<Buf> bufs;  // per task, reused across POCs
+  // deferred mode (vame_log_writer_set_deferred): each file's rows held in
+  // memory, in blocks, until vame_log_writer_flush_at places them
+  struct Held {
+    std::vector<std::unique_ptr<char[]>> blocks;
+    size_t last = 0;   // bytes used in the last block
+    long long total = 0;
+  };
+  static constexpr size_t kHeldBlock = size_t(32) << 20;
+  bool deferred = false;
+  std::vector<Held> held;
   ~vame_log_writer() {
     for (int fd : fds)
       if (fd >= 0) close(fd);
@@ -434,6 +444,27 @@ long long vame_log_writer_refs(vame_log_writer* w, int poc, int ref0, int nrefs,
   std::atomic<int> bad{0};
   w->pool->run((int)w->paths.size(), [&](int f) {
     if (per[f].empty()) return;
+    if (w->deferred) {  // into the file's held blocks, in order
+      vame_log_writer::Held& h = w->held[f];
+      for (int i : per[f]) {
+        const char* q = w->bufs[i].d.get();
+        size_t left = w->bufs[i].len;
+        wrote[f] += (long long)left;
+        h.total += (long long)left;
+        while (left) {
+          if (h.blocks.empty() || h.last == vame_log_writer::kHeldBlock) {
+            h.blocks.emplace_back(new char[vame_log_writer::kHeldBlock]);
+            h.last = 0;
+          }
+          const size_t k = std::min(left, vame_log_writer::kHeldBlock - h.last);
+          memcpy(h.blocks.back().get() + h.last, q, k);
+          h.last += k;
+          q += k;
+          left -= k;
+        }
+      }
+      return;
+    }
     int& fd = w->fds[f];
     if (fd < 0) fd = open(w->paths[f].c_str(), O_WRONLY | O_APPEND | O_CREAT, 0644);
     if (fd < 0) {
@@ -481,6 +512,64 @@ long long vame_log_writer_refs(vame_log_writer* w, int poc, int ref0, int nrefs,
   return total;
 }
 
+int vame_log_writer_set_deferred(vame_log_writer* w, int deferred) {
+  if (!w) return VAME_E_INVALID;
+  w->deferred = deferred != 0;
+  w->held.resize(w->paths.size());
+  return VAME_OK;
+}
+
+int vame_log_writer_num_files(vame_log_writer* w) { return w ? (int)w->paths.size() : VAME_E_INVALID; }
+
+int vame_log_writer_file_name(vame_log_writer* w, int f, char* buf, int buflen) {
+  if (!w || f < 0 || f >= (int)w->paths.size() || !buf || buflen <= (int)w->paths[f].size())
+    return VAME_E_INVALID;
+  memcpy(buf, w->paths[f].c_str(), w->paths[f].size() + 1);
+  return VAME_OK;
+}
+
+int vame_log_writer_sizes(vame_log_writer* w, long long* sizes) {
+  if (!w || !sizes) return VAME_E_INVALID;
+  for (size_t f = 0; f < w->paths.size(); f++) sizes[f] = f < w->held.size() ? w->held[f].total : 0;
+  return VAME_OK;
+}
+
+long long vame_log_writer_flush_at(vame_log_writer* w, const long long* offsets) {
+  if (!w || !offsets) return VAME_E_INVALID;
+  std::atomic<int> bad{0};
+  std::atomic<long long> total{0};
+  w->held.resize(w->paths.size());
+  w->pool->run((int)w->paths.size(), [&](int f) {
+    vame_log_writer::Held& h = w->held[f];
+    if (!h.total) return;
+    const int fd = open(w->paths[f].c_str(), O_WRONLY | O_CREAT, 0644);  // never truncated
+    if (fd < 0) {
+      bad = 1;
+      return;
+    }
+    long long off = offsets[f];
+    for (size_t b = 0; b < h.blocks.size(); b++) {
+      const char* q = h.blocks[b].get();
+      size_t left = b + 1 == h.blocks.size() ? h.last : vame_log_writer::kHeldBlock;
+      while (left) {
+        const ssize_t k = pwrite(fd, q, left, (off_t)off);
+        if (k <= 0) {
+          bad = 1;
+          close(fd);
+          return;
+        }
+        q += k;
+        off += k;
+        left -= (size_t)k;
+      }
+    }
+    close(fd);
+    total += h.total;
+    h = vame_log_writer::Held();
+  });
+  return bad ? VAME_E_INVALID : total.load();
+}
+
 int vame_log_writer_destroy(vame_log_writer* w) {
   delete w;
   return VAME_OK;
@@ -493,8 +582,42 @@ int vame_read_frames(const char* path, int width, int height, int nframes, uint1
 
 int vame_read_frames_range(const char* path, int width, int height, int first_frame, int nframes,
                            uint16_t* out, int nthreads) {
+  return vame_read_frames_span(path, width, height, first_frame, nframes, 0, 0, -1, out, nthreads);
+}
+
+long long vame_count_lines(const char* path, long long begin, long long end, int nthreads) {
+  if (!path || begin < 0) return VAME_E_INVALID;
+  Mapped m;
+  if (int rc = map_file(path, m)) return rc;
+  const size_t e = end < 0 ? m.n : std::min((size_t)end, m.n);
+  if ((size_t)begin >= e) return 0;
+  const size_t len = e - (size_t)begin;
+  const int T = pick_threads(nthreads, (long)(len >> 20) + 1);
+  std::vector<long long> nl(T, 0);
+  parallel_for(T, T, [&](int t, int) {
+    const char* q = m.p + begin + len * t / T;
+    const char* qe = m.p + begin + len * (t + 1) / T;
+    long long c = 0;
+    while (q < qe) {
+      const char* r = (const char*)memchr(q, '\n', (size_t)(qe - q));
+      if (!r) break;
+      c++;
+      q = r + 1;
+    }
+    nl[t] = c;
+  });
+  long long c = 0;
+  for (long long v : nl) c += v;
+  return c;
+}
+
+int vame_read_frames_span(const char* path, int width, int height, int first_frame, int nframes,
+                          long long span_begin, long long lines_before, long long span_end,
+                          uint16_t* out, int nthreads) {
   const int first = first_frame;
-  if (!path || !out || width <= 0 || height <= 0 || first < 0 || nframes <= 0) return VAME_E_INVALID;
+  if (!path || !out || width <= 0 || height <= 0 || first < 0 || nframes <= 0 || span_begin < 0 ||
+      lines_before < 0)
+    return VAME_E_INVALID;
   Mapped m;
   int rc = map_file(path, m);
   if (rc) return rc;
@@ -504,16 +627,19 @@ int vame_read_frames_range(const char* path, int width, int height, int first_fr
     memcpy(out, m.p + fsz * first * 2, fsz * nframes * 2);
     return VAME_OK;
   }
-  // text lines [line0, nlines) are frames first .. first + nframes - 1
+  // text lines [line0, nlines) are frames first .. first + nframes - 1; the
+  // bytes [b0, n) hold them, with lines_before newlines ahead of b0
   const long line0 = (long)first * height;
   const long nlines = ((long)first + nframes) * height;
   const char* base = m.p;
-  const size_t n = m.n;
-  if (n == 0) return VAME_E_INVALID;
+  const size_t n = span_end < 0 ? m.n : std::min((size_t)span_end, m.n);
+  const size_t b0 = (size_t)span_begin;
+  if (m.n == 0 || b0 >= n || line0 < lines_before) return VAME_E_INVALID;
+  const size_t len = n - b0;
   // pass 1: newline count per byte range
-  const int T = pick_threads(nthreads, (long)(n >> 20) + 1);
+  const int T = pick_threads(nthreads, (long)(len >> 20) + 1);
   std::vector<size_t> cut(T + 1);
-  for (int t = 0; t <= T; t++) cut[t] = n * t / T;
+  for (int t = 0; t <= T; t++) cut[t] = b0 + len * t / T;
   std::vector<long> nl(T, 0);
   parallel_for(T, T, [&](int t, int) {
     long c = 0;
@@ -525,28 +651,26 @@ int vame_read_frames_range(const char* path, int width, int height, int first_fr
     }
     nl[t] = c;
   });
-  // line index of the first line starting in range t: lines start at 0 and after each '\n'
-  std::vector<long> firstLine(T + 1, 0);
+  // the line that holds byte cut[t] (lines start at 0 and after each '\n')
+  std::vector<long> firstLine(T + 1, (long)lines_before);
   for (int t = 0; t < T; t++) firstLine[t + 1] = firstLine[t] + nl[t];
-  const long total_lines = firstLine[T] + (base[n - 1] != '\n' ? 1 : 0);
+  const long total_lines = firstLine[T] + (n == m.n && base[n - 1] != '\n' ? 1 : 0);
   if (total_lines < nlines) return VAME_E_INVALID;
-  // pass 2: parse the lines that START in each range (line 0 starts at byte 0)
+  // pass 2: parse the lines that START in each range
   std::vector<int> bad(T, 0);
   parallel_for(T, T, [&](int t, int) {
     const char* q = base + cut[t];
     long li = firstLine[t];
-    if (t > 0) {  // skip the tail of a line started in an earlier range
-      if (base[cut[t] - 1] != '\n') {
-        const char* r = (const char*)memchr(q, '\n', (size_t)(base + cut[t + 1] - q));
-        if (!r) return;
-        q = r + 1;
-        li++;  // firstLine[t] is the line that straddles cut[t]; q starts the next one
-      }
+    if (cut[t] > 0 && base[cut[t] - 1] != '\n') {  // skip the tail of a line started earlier
+      const char* r = (const char*)memchr(q, '\n', (size_t)(base + cut[t + 1] - q));
+      if (!r) return;
+      q = r + 1;
+      li++;  // firstLine[t] is the line that straddles cut[t]; q starts the next one
     }
     const char* end = base + cut[t + 1];
     while (q < end && li < nlines) {
-      const char* r = (const char*)memchr(q, '\n', (size_t)(base + n - q));
-      const char* le = r ? r : base + n;
+      const char* r = (const char*)memchr(q, '\n', (size_t)(base + m.n - q));
+      const char* le = r ? r : base + m.n;
       if (li >= line0 && !parse_line(q, le, width, out + (size_t)(li - line0) * width)) {
         bad[t] = 1;
         return;

@@ -16,7 +16,9 @@ EXPORTS = (
     "vame_get_timing", "vame_read_frames", "vame_log_remove_old", "vame_log_write_headers",
     "vame_log_append", "vame_log_file_count", "vame_set_prof", "vame_affine_me_batch",
     "vame_log_writer_create", "vame_log_writer_poc", "vame_log_writer_destroy", "vame_pred_mask",
-    "vame_log_writer_refs", "vame_read_frames_range",
+    "vame_log_writer_refs", "vame_read_frames_range", "vame_count_lines", "vame_read_frames_span",
+    "vame_log_writer_set_deferred", "vame_log_writer_num_files", "vame_log_writer_file_name",
+    "vame_log_writer_sizes", "vame_log_writer_flush_at",
 )
 
 
@@ -69,6 +71,10 @@ def lib():
         C = ctypes.c_char_p
         L.vame_read_frames.argtypes = [C, I, I, I, P, I]
         L.vame_read_frames_range.argtypes = [C, I, I, I, I, P, I]
+        LL = ctypes.c_longlong
+        L.vame_count_lines.argtypes = [C, LL, LL, I]
+        L.vame_count_lines.restype = LL
+        L.vame_read_frames_span.argtypes = [C, I, I, I, I, LL, LL, LL, P, I]
         L.vame_log_remove_old.argtypes = [C]
         L.vame_log_write_headers.argtypes = [C, I]
         L.vame_log_append.argtypes = [C, I, I, I, I, I, P, P, I]
@@ -81,6 +87,12 @@ def lib():
         L.vame_log_writer_refs.argtypes = [P, I, I, I, I, P, P]
         L.vame_log_writer_refs.restype = ctypes.c_longlong
         L.vame_log_writer_destroy.argtypes = [P]
+        L.vame_log_writer_set_deferred.argtypes = [P, I]
+        L.vame_log_writer_num_files.argtypes = [P]
+        L.vame_log_writer_file_name.argtypes = [P, I, ctypes.c_char_p, I]
+        L.vame_log_writer_sizes.argtypes = [P, P]
+        L.vame_log_writer_flush_at.argtypes = [P, P]
+        L.vame_log_writer_flush_at.restype = ctypes.c_longlong
         _lib = L
     return _lib
 

@@ -17,11 +17,12 @@ next one.  The logs are written in the reference's order by one of two paths:
                 compactly on its GPU (`shard.pack`), and after the last launch
                 one gather (RCCL over xGMI) brings them to rank 0, which writes
                 them POC by POC.  Rank 0's CPU formats the whole log.
-  --shard-logs  every rank formats its own block (rank 0 into the final files,
-                rank k into part files `<prefix>.partK_*`) as it completes; at
-                the end the ranks exchange the part sizes and copy their parts
-                into the final files at their offsets in parallel
-                (copy_file_range), so formatting scales with the ranks.
+  --shard-logs  every rank formats its own block as it completes -- rank 0
+                into the final files, rank k into host memory (a deferred
+                `vame_log_writer`) -- and at the end the ranks exchange their
+                byte counts per file (one all_reduce) and write their blocks
+                into the final files at their offsets, all ranks in parallel
+                (pwrite), so formatting and writing scale with the ranks.
 
 Blocks are contiguous in coding order, and a POC cut between two ranks is cut
 at a refIdx boundary (refIdx is the outer loop of every file's rows), so both
@@ -134,30 +135,40 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
         if dist is not None:
             dist.barrier()
 
-    # ---- frame ingest: only the frames this block reads (main.cpp:293-330)
+    # ---- frame ingest: only the frames this block reads (main.cpp:293-330).
+    # Text lines have no fixed length, so the ranks first index the CSVs
+    # together: rank r counts the newlines of chunks r, r + N, ... and one
+    # all_reduce shares the counts; each rank then parses only the chunks that
+    # hold its frames.
     t = time.perf_counter()
+    idx = {path: line_index(path, world, rank, dist, T) for path in (a.orig, a.recon)}
     d_orig, d_recon = {}, {}
     if blocks:
         pocs = [p for p, _ in blocks]
         need = sorted({ref_list(p)[r] for p, refs in blocks for r in refs})
-        orig = logs.read_frames(a.orig, W, H, pocs[-1] - pocs[0] + 1, first=pocs[0] - 1)
-        recon = logs.read_frames(a.recon, W, H, need[-1] - need[0] + 1, first=need[0])
-        T["read_csv_s"] = time.perf_counter() - t
+
+        def read(path, first, n):
+            span = None if idx[path] is None else logs.line_span(*idx[path], first * H, (first + n) * H)
+            return logs.read_frames(path, W, H, n, first=first, span=span)
+        orig = read(a.orig, pocs[0] - 1, pocs[-1] - pocs[0] + 1)
+        recon = read(a.recon, need[0], need[-1] - need[0] + 1)
+    T["read_csv_s"] = time.perf_counter() - t - T.get("index_others_s", 0.0)
+    if blocks:
         up = lambda f: torch.from_numpy(np.ascontiguousarray(f).view(np.int16)).to(device)  # noqa: E731
         d_orig = {p: up(orig[p - pocs[0]]) for p in pocs}
         d_recon = {q: up(recon[q - need[0]]) for q in need}
         del orig, recon
 
-    # ---- who writes what
+    # ---- who writes what: rank 0 appends to the final files as it goes; with
+    # --shard-logs every other rank formats its block into host memory (a
+    # deferred writer) and places it into the same files at the end
     writes_own = bool(a.log) and (rank == 0 or a.shard_logs)
-    prefix = a.log if rank == 0 else part_prefix(a.log, rank)
+    prefix = a.log if (rank == 0 or dist is not None) else part_prefix(a.log, rank)  # --rank-only K: parts
     if a.log and rank == 0:
         logs.remove_old(a.log)  # removeOldTraces (main.cpp:469)
-    if writes_own and rank > 0:
-        for name in logs.log_names(prefix):
-            if os.path.exists(name):
-                os.remove(name)
     writer = logs.LogWriter(prefix, W, H) if writes_own else None
+    if writer is not None and rank > 0:
+        writer.defer()
     slab_parts = []
 
     # ---- the writer thread: formats each launch's POCs once its copy landed
@@ -257,54 +268,71 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
                     T["log_bytes"] += logs.write_poc(prefix, W, H, poc, results, writer=writer)
             T["log_write_s"] += time.perf_counter() - t0
         del slabs
-    if writer is not None:
+    if writer is not None and rank == 0:
         writer.close()
 
-    # ---- --shard-logs: the parts into the final files, every rank in parallel
-    if world > 1 and a.log and a.shard_logs and dist is not None:
-        barrier()
+    # ---- --shard-logs: every rank's block into the final files at its byte
+    # offsets (the sizes of the ranks before it), all ranks in parallel
+    if writer is not None and rank > 0:
         t = time.perf_counter()
-        names = logs.log_names(a.log, pred_mask(modes))
-        size = lambda p: os.path.getsize(p) if os.path.exists(p) else 0  # noqa: E731
-        base = {n: size(n) for n in names}
-        parts = {n: [size(part_prefix(a.log, r) + n[len(a.log):]) for r in range(1, world)] for n in names}
-        barrier()  # every rank has read rank 0's sizes before rank 0 grows the files
-        if rank == 0:
-            for n in names:
-                if base[n] or any(parts[n]):
-                    with open(n, "ab") as f:
-                        f.truncate(base[n] + sum(parts[n]))
-        barrier()
-        if rank > 0:
-            for n in names:
-                src = part_prefix(a.log, rank) + n[len(a.log):]
-                if parts[n][rank - 1]:
-                    _copy_into(src, n, base[n] + sum(parts[n][:rank - 1]))
-                if os.path.exists(src):
-                    os.remove(src)
-        barrier()
+        held = writer.held_sizes()
+        if dist is None:  # --rank-only K: its block alone, into its part files
+            offsets = [0] * len(held)
+        else:
+            names = writer.files()
+            sizes = torch.zeros((world, len(names)), dtype=torch.int64)
+            sizes[rank] = torch.tensor(held, dtype=torch.int64)
+            _all_reduce_cpu(dist, sizes)
+            offsets = sizes[:rank].sum(0).tolist()
+        writer.flush_at(offsets)
+        writer.close()
         T["merge_s"] = time.perf_counter() - t
+    elif world > 1 and a.log and a.shard_logs and dist is not None and rank == 0:
+        names = logs.log_names(a.log)
+        sizes = torch.zeros((world, len(names)), dtype=torch.int64)
+        sizes[0] = torch.tensor([os.path.getsize(n) if os.path.exists(n) else 0 for n in names])
+        _all_reduce_cpu(dist, sizes)
+    if world > 1 and a.log and a.shard_logs and dist is not None:
+        barrier()  # every block is in place
     T["overall_s"] = time.perf_counter() - t_start
     return T
 
 
-def _copy_into(src: str, dst: str, offset: int) -> None:
-    """All of `src` into `dst` at `offset` (in-kernel copy; plain reads and
-    positioned writes where the file system refuses copy_file_range)."""
-    with open(src, "rb") as s, open(dst, "r+b") as d:
-        n = os.fstat(s.fileno()).st_size
-        done = 0
-        try:
-            while done < n:
-                k = os.copy_file_range(s.fileno(), d.fileno(), n - done, done, offset + done)
-                if k <= 0:
-                    raise OSError("copy_file_range made no progress")
-                done += k
-        except OSError:
-            while done < n:
-                chunk = os.pread(s.fileno(), min(64 << 20, n - done), done)
-                os.pwrite(d.fileno(), chunk, offset + done)
-                done += len(chunk)
+def line_index(path: str, world: int, rank: int, dist, T: dict):
+    """(chunk byte bounds, newline prefix counts) of a CSV, or None for raw
+    frames / a one-rank run (which reads its frames from the start).  Rank r
+    counts chunks r, r + world, ...; an all_reduce sums the counts.  Without
+    a process group (--rank-only) the other ranks' chunks are counted here too,
+    and that time is kept apart (T["index_others_s"]): on a node those chunks
+    are counted by the other ranks, at the same time."""
+    if world == 1 or path.endswith((".u16", ".yuv")):
+        return None
+    size = os.path.getsize(path)
+    K = max(world, min(64 * world, size >> 22))  # chunks of >= 4 MiB
+    bounds = [size * k // K for k in range(K + 1)]
+    counts = torch.zeros(K, dtype=torch.int64)
+    for k in range(rank, K, world):
+        counts[k] = logs.count_lines(path, bounds[k], bounds[k + 1])
+    if dist is not None:
+        _all_reduce_cpu(dist, counts)
+    else:
+        t = time.perf_counter()
+        for k in range(K):
+            if k % world != rank:
+                counts[k] = logs.count_lines(path, bounds[k], bounds[k + 1])
+        T["index_others_s"] = T.get("index_others_s", 0.0) + time.perf_counter() - t
+    prefix = [0] + torch.cumsum(counts, 0).tolist()
+    return bounds, prefix
+
+
+def _all_reduce_cpu(dist, t: torch.Tensor) -> None:
+    """Sum a small CPU tensor over the ranks (through the GPU under RCCL)."""
+    if dist.get_backend() == "nccl":
+        c = t.cuda()
+        dist.all_reduce(c)
+        t.copy_(c.cpu())
+    else:
+        dist.all_reduce(t)
 
 
 def report(a, per_rank: list[dict]) -> str:

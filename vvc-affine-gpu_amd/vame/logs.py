@@ -16,16 +16,41 @@ CPMVS_DTYPE = np.dtype([("nCPs", "<i4"), ("LTx", "<i4"), ("LTy", "<i4"), ("RTx",
 
 
 def read_frames(path: str, width: int, height: int, n_frames: int, nthreads: int = 0,
-                first: int = 0) -> np.ndarray:
+                first: int = 0, span=None) -> np.ndarray:
     """(n_frames, H, W) uint16 from a reference-layout CSV (or raw .u16/.yuv):
-    frames first .. first + n_frames - 1 of the file."""
+    frames first .. first + n_frames - 1 of the file.  span = (begin,
+    lines_before, end): only bytes [begin, end) are read (see line_span)."""
     out = np.empty((n_frames, height, width), np.uint16)
-    rc = lib().vame_read_frames_range(path.encode(), width, height, first, n_frames,
-                                      out.ctypes.data_as(ctypes.c_void_p), nthreads)
+    b, lb, e = span if span is not None else (0, 0, -1)
+    rc = lib().vame_read_frames_span(path.encode(), width, height, first, n_frames, b, lb, e,
+                                     out.ctypes.data_as(ctypes.c_void_p), nthreads)
     if rc != 0:
         raise VameError(f"cannot read frames {first}..{first + n_frames - 1} of {width}x{height} "
                         f"from {path} (rc={rc})")
     return out
+
+
+def count_lines(path: str, begin: int = 0, end: int = -1, nthreads: int = 0) -> int:
+    """Number of '\\n' in bytes [begin, end) of a file (end < 0: to the end)."""
+    n = lib().vame_count_lines(path.encode(), begin, end, nthreads)
+    if n < 0:
+        raise VameError(f"cannot read {path}")
+    return n
+
+
+def line_span(bounds: list[int], prefix: list[int], line0: int, line1: int) -> tuple[int, int, int]:
+    """(begin, lines_before, end) of the chunks that hold text lines [line0,
+    line1), from chunk byte bounds[0..K] and prefix[k] = the newlines ahead of
+    bounds[k] (line L starts after newline L - 1)."""
+    import bisect
+    K = len(bounds) - 1
+    if line0 == 0:
+        b, lb = 0, 0
+    else:
+        k0 = min(bisect.bisect_right(prefix, line0 - 1) - 1, K - 1)
+        b, lb = bounds[k0], prefix[k0]
+    k1 = bisect.bisect_right(prefix, line1 - 1) - 1  # chunk of the last line's newline
+    return b, lb, bounds[min(k1 + 1, K)]
 
 
 def log_names(prefix: str, pred_mask: int = 15) -> list[str]:
@@ -118,6 +143,36 @@ class LogWriter:
         nb = lib().vame_log_writer_refs(self._w, poc, r0, len(refs), mask, cost_p, cp_p)
         if nb < 0:
             raise VameError("writing the log files failed")
+        return nb
+
+    def defer(self) -> None:
+        """Keep the rows in memory (vame_log_writer_set_deferred) until flush_at."""
+        if lib().vame_log_writer_set_deferred(self._w, 1) != 0:
+            raise VameError("vame_log_writer_set_deferred failed")
+
+    def files(self) -> list[str]:
+        """The writer's files, in its numbering."""
+        L = lib()
+        buf = ctypes.create_string_buffer(4096)
+        out = []
+        for f in range(L.vame_log_writer_num_files(self._w)):
+            if L.vame_log_writer_file_name(self._w, f, buf, len(buf)) != 0:
+                raise VameError("vame_log_writer_file_name failed")
+            out.append(buf.value.decode())
+        return out
+
+    def held_sizes(self) -> list[int]:
+        n = lib().vame_log_writer_num_files(self._w)
+        arr = (ctypes.c_longlong * n)()
+        lib().vame_log_writer_sizes(self._w, arr)
+        return list(arr)
+
+    def flush_at(self, offsets: list[int]) -> int:
+        """Write every file's held rows at offsets[f] (vame_log_writer_flush_at)."""
+        arr = (ctypes.c_longlong * len(offsets))(*offsets)
+        nb = lib().vame_log_writer_flush_at(self._w, arr)
+        if nb < 0:
+            raise VameError("vame_log_writer_flush_at failed")
         return nb
 
     def close(self) -> None:
