@@ -70,6 +70,9 @@ def main():
     ap.add_argument("--frames", type=int, default=None,
                     help="sequence length (c5: total POCs; c2-c4: POCs per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rank-only", type=int, default=None, metavar="K",
+                    help="diagnostic: run only rank K's block of a --gpus N job, alone on GPU 0 "
+                         "(no process group, no gather): one rank of an N-GPU node, priced on one GPU")
     ap.add_argument("--no-spans", action="store_true",
                     help="skip the per-POC span step (profiling runs: identical launches only)")
     args = ap.parse_args()
@@ -85,7 +88,10 @@ def main():
         sys.exit("bench.py: --gpus must be >= 1")
     from vame.launch import init_rank, launch_ranks
     backend = os.environ.get("VAME_DIST_BACKEND", "nccl")
-    if "WORLD_SIZE" not in os.environ:
+    if args.rank_only is not None:
+        if not 0 <= args.rank_only < args.gpus or "WORLD_SIZE" in os.environ:
+            sys.exit("bench.py: --rank-only K needs 0 <= K < --gpus and no launcher")
+    elif "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:  # no launcher: start the N ranks here (nothing has touched the GPU yet)
             sys.exit(launch_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:], backend,
                                   "bench.py"))
@@ -93,6 +99,8 @@ def main():
         sys.exit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher but --gpus {args.gpus}")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     dist, rank, dev = init_rank(world, backend)
+    if args.rank_only is not None:  # shard as N ranks, run rank K's block only
+        world, rank = args.gpus, args.rank_only
 
     from vame.engine import Engine
     from vame.metrics import pair_accounting
@@ -168,13 +176,20 @@ def main():
     value = rows_total / tmax
 
     # the one exchange step, outside the timed steps: decision records to rank 0
+    # (a --rank-only diagnostic has no other ranks: it checks its own block)
     barrier()
     tg = time.perf_counter()
-    slabs, gather_bytes = run.gather()
+    if args.rank_only is None:
+        slabs, gather_bytes = run.gather()
+    else:
+        slabs, gather_bytes = None, 0
     torch.cuda.synchronize()
     gather_ms = (time.perf_counter() - tg) * 1e3
     gather_ms = all_reduce([gather_ms], ops and ops.MAX)[0]
-    check = run.verify(slabs) if rank == 0 else None
+    if args.rank_only is not None:
+        check = run.verify_own()
+    else:
+        check = run.verify(slabs) if rank == 0 else None
     del slabs
 
     # roofline of the dominant kernel (quadrant work items, affine_me_quad)
@@ -190,7 +205,7 @@ def main():
         "metric": "candidate CU-blocks/s at 1080p QP32; bit-exact CPMV/cost match vs reference",
         "value": value,
         "unit": "CU-blocks/s",
-        "n_gpus": world,
+        "n_gpus": 1 if args.rank_only is not None else world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": tmax * 1e3 / args.steps,
@@ -209,7 +224,8 @@ def main():
                    "pairs_per_step_rank0": run.pairs, "rows_per_step_rank0": rows_per_step,
                    "rows_per_step_all": rows_total / args.steps,
                    "modes": "2cp+3cp" if modes & 2 else "2cp",
-                   "parallelism": f"frame-shard x{world} (pair_shard of one sequence)"},
+                   "parallelism": f"frame-shard x{world} (pair_shard of one sequence)",
+                   **({"rank_only": {"rank": rank, "of": world}} if args.rank_only is not None else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": prof.get("traffic"),
                      "kernel": "affine_me_quad",

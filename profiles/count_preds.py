@@ -30,6 +30,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--qp", type=int, default=None)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--rank-only", type=int, default=0, help="count rank K's block of a --gpus N job")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     qp = cfg["qp"] if args.qp is None else args.qp
@@ -40,7 +42,13 @@ def main():
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     eng = Engine(cfg["W"], cfg["H"], 0)
-    run = ShardRun(eng, cfg["W"], cfg["H"], qp, cfg["frames"], cfg["modes"], 1, 0, dev)
+    n_pairs = None
+    if cfg["scaling"] == "weak":  # bench.py's weak-scaling prefix of the sequence
+        from vame.shard import frames_for_pairs, sequence_pairs
+        n_pairs = sequence_pairs(cfg["frames"]) * args.gpus
+    frames = cfg["frames"] if n_pairs is None else frames_for_pairs(n_pairs)
+    run = ShardRun(eng, cfg["W"], cfg["H"], qp, frames, cfg["modes"], args.gpus, args.rank_only, dev,
+                   n_pairs=n_pairs)
     cnt = (ctypes.c_ulonglong * 4)()
     L.vame_debug_pred_count(cnt, 1)
     run.step()
@@ -48,7 +56,7 @@ def main():
     L.vame_debug_pred_count(cnt, 1)
     acc = pair_accounting(cfg["W"], cfg["H"], (2, 3) if cfg["modes"] & 2 else (2,))
     alg_q, alg_b = acc["sb_pred_quad"] * run.pairs, acc["sb_pred_big"] * run.pairs
-    out = {"config": args.config, "qp": qp, "pairs": run.pairs,
+    out = {"config": args.config, "qp": qp, "pairs": run.pairs, "rank": [args.rank_only, args.gpus],
            "executed_quad": cnt[0], "algorithmic_quad": alg_q, "executed_pred_frac_quad": cnt[0] / alg_q,
            "executed_ctu": cnt[1], "algorithmic_ctu": alg_b, "executed_pred_frac_ctu": cnt[1] / alg_b,
            "executed_pred_frac": (cnt[0] + cnt[1]) / (alg_q + alg_b),

@@ -33,7 +33,7 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU S
 echo "[prof] prediction count"
 if [ -f $R/vvc-affine-gpu_amd/lib/libvame_count.so ]; then
   VAME_LIB=$R/vvc-affine-gpu_amd/lib/libvame_count.so timeout -k 10 300 \
-      python3 $R/profiles/count_preds.py --config $CFG > $O/count.json 2> $O/count.err
+      python3 $R/profiles/count_preds.py --config $CFG ${COUNT_ARGS:-} > $O/count.json 2> $O/count.err
   cat $O/count.json
 fi
 python3 $R/profiles/pmc_summary.py $O $O/summary.json > /dev/null

@@ -328,3 +328,16 @@ def test_bench_shard_path_two_ranks_equals_single_process(tmp_path):
         ofs += n
     assert ofs == whole.numel()
     assert got["bytes"] == 4 * got["slabs"][0].numel()
+
+
+@pytest.mark.timeout(300)
+def test_rank_only_block_and_verify_own():
+    """A --rank-only diagnostic (bench.py / vame.distrun): rank 1's block of a
+    2-rank job run alone, no process group; verify_own recomputes its first and
+    last block entry and matches its own records."""
+    from vame.seqrun import ShardRun
+    run = ShardRun(OracleEngine(SEQ_W, SEQ_H), SEQ_W, SEQ_H, 27, SEQ_N, 3, 2, 1, torch.device("cpu"), seed=11)
+    assert run.blocks == shard.pair_shard(SEQ_N, 2, 1)
+    run.step()
+    chk = run.verify_own()
+    assert chk["byte_identical"] and [p for p, _, _ in chk["pocs"]] == [4, 5]

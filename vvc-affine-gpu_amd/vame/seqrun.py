@@ -84,6 +84,19 @@ class ShardRun:
         slabs = shard.gather_to_root(slab, self.world, 0)
         return slabs, 4 * self.words * (self.world - 1)
 
+    def verify_own(self) -> dict:
+        """This rank's first and last block entry recomputed and compared with
+        the records of its own last step (no gather: a --rank-only run)."""
+        if not self.blocks:
+            return {"pocs": [], "byte_identical": True}
+        idx = sorted({0, len(self.blocks) - 1})
+        sample = [self.blocks[i] for i in idx]
+        jobs = self._jobs(sample)
+        self.eng.affine_me_batch(jobs, self.modes, 0)
+        ok = all(torch.equal(shard.pack([j[3]], modes=self.modes), shard.pack([self.jobs[i][3]], modes=self.modes))
+                 for i, j in zip(idx, jobs))
+        return {"pocs": [[p, r, self.rank] for p, r in sample], "byte_identical": ok}
+
     def cut_pocs(self) -> list[int]:
         """POCs whose refIdx range is split between two ranks' pair blocks."""
         owners: dict[int, set] = {}
