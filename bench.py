@@ -258,7 +258,7 @@ def main():
         result["cpu_baseline"], result["parity_sample"] = cpu_baseline(run, acc, ncps, W, H, modes)
     if dist is not None:
         dist.barrier()
-    if rank == 0:
+    if rank == 0 or args.rank_only is not None:
         print(json.dumps(result), flush=True)
     eng.close()
     if dist is not None:

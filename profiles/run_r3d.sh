@@ -1,8 +1,13 @@
 set -o pipefail
 O=gpurun_out/r3d; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+tail -2 $O/pytest_gpu.log
 for c in c2 c3 c4; do
-  bash profiles/run_profile.sh $c $c 2>&1 | tail -3 | tee $O/prof_$c.txt || exit 1
+  bash profiles/heartbeat.sh bash profiles/run_profile.sh $c $c > $O/prof_$c.txt 2>&1 || { tail -20 $O/prof_$c.txt; exit 1; }
+  tail -2 $O/prof_$c.txt
 done
+VAME_LIB=vvc-affine-gpu_amd/lib/libvame_count.so timeout -k 10 300 python3 profiles/count_preds.py --config c5 --gpus 8 --rank-only 7 > gpurun_out/prof_c5r7/count.json 2> $O/count_c5r7.err || { tail $O/count_c5r7.err; exit 1; }
+cat gpurun_out/prof_c5r7/count.json
+timeout -k 10 300 python3 bench.py --config c5 --gpus 8 --rank-only 7 > gpurun_out/prof_c5r7/bench.json 2> $O/bench_c5r7.err || exit 1
 VAME_LIB=vvc-affine-gpu_amd/lib/libvame_phase.so timeout -k 10 300 python3 profiles/phase_profile.py --config c4 --steps 1 > $O/phase_c4.txt 2>&1 || exit 1
-VAME_LIB=vvc-affine-gpu_amd/lib/libvame_phase.so timeout -k 10 300 python3 profiles/phase_profile.py --config c2 --steps 5 > $O/phase_c2.txt 2>&1 || exit 1
 cat $O/phase_c4.txt
