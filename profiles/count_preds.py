@@ -49,7 +49,7 @@ def main():
     frames = cfg["frames"] if n_pairs is None else frames_for_pairs(n_pairs)
     run = ShardRun(eng, cfg["W"], cfg["H"], qp, frames, cfg["modes"], args.gpus, args.rank_only, dev,
                    n_pairs=n_pairs)
-    cnt = (ctypes.c_ulonglong * 4)()
+    cnt = (ctypes.c_ulonglong * 6)()
     L.vame_debug_pred_count(cnt, 1)
     run.step()
     torch.cuda.synchronize()
@@ -61,7 +61,9 @@ def main():
            "executed_ctu": cnt[1], "algorithmic_ctu": alg_b, "executed_pred_frac_ctu": cnt[1] / alg_b,
            "executed_pred_frac": (cnt[0] + cnt[1]) / (alg_q + alg_b),
            # executed predictions whose 9x9 window left the staged tile (clamped global loads)
-           "outside_tile_frac_quad": cnt[2] / max(cnt[0], 1), "outside_tile_frac_ctu": cnt[3] / max(cnt[1], 1)}
+           "outside_tile_frac_quad": (cnt[2] + cnt[3]) / max(cnt[0], 1),
+           "outside_tile_frac_ctu": (cnt[4] + cnt[5]) / max(cnt[1], 1),
+           "outside_tile_quad_2cp_3cp": [cnt[2], cnt[3]], "outside_tile_ctu_2cp_3cp": [cnt[4], cnt[5]]}
     print(json.dumps(out))
     eng.close()
 

@@ -637,13 +637,14 @@ int vame_debug_phase_cycles(unsigned long long* out32, int reset) {
 #endif
 #if VAME_COUNT_PRED
 // instrumentation builds: sub-block predictions run, [quad, ctu], and those of
-// them whose window left the staged tile, [2 + quad, 2 + ctu] (see vame_kernel.h)
-int vame_debug_pred_count(unsigned long long* out4, int reset) {
-  if (!out4) return VAME_E_INVALID;
+// them whose window left the staged tile, [2 + quad 2-CP, quad 3-CP, ctu 2-CP,
+// ctu 3-CP] (see vame_kernel.h)
+int vame_debug_pred_count(unsigned long long* out6, int reset) {
+  if (!out6) return VAME_E_INVALID;
   VAME_HIP(hipDeviceSynchronize());
-  VAME_HIP(hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_pred_count), sizeof(unsigned long long) * 4));
+  VAME_HIP(hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_pred_count), sizeof(unsigned long long) * 6));
   if (reset) {
-    unsigned long long z[4] = {};
+    unsigned long long z[6] = {};
     VAME_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pred_count), z, sizeof(z)));
   }
   return VAME_OK;

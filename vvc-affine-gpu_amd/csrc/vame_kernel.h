@@ -106,7 +106,7 @@ struct KParams {
 // bit 1 skip the gradient math, bit 2 skip the reductions of the equations,
 // bit 3 skip the prediction math, bit 4 skip the 128-class launch, bit 5 skip
 // the quadrant launch, bit 8 (host) 128-class templates without the 128x64 /
-// 64x128 items.
+// 64x128 items, bit 9 every 9x9 window read from the tile (no clamped-global path).
 #ifndef VAME_ABLATE
 #define VAME_ABLATE 0
 #endif
@@ -117,6 +117,17 @@ struct KParams {
 #ifndef VAME_DUP
 #define VAME_DUP 0
 #endif
+// Wide, batched loads for windows outside the staged tile (filter_rows_global).
+#ifndef VAME_WIDE_GLOBAL
+#define VAME_WIDE_GLOBAL 1
+#endif
+#ifndef VAME_GLOBAL_BATCH
+#define VAME_GLOBAL_BATCH 5
+#endif
+// One filter pass for a whole wave whose windows partly leave the tile.
+#ifndef VAME_MIXED_FILTER
+#define VAME_MIXED_FILTER 1
+#endif
 // Wave priority (s_setprio) during the latency-bound solve: its dependent
 // FP64 / LDS chain issues ahead of other waves' prediction work (~0.5 %;
 // priority 1 / 3 and priority over the whole post-prediction part measured
@@ -126,12 +137,13 @@ constexpr int kSolvePrio = 3;
 // VAME_COUNT_PRED (instrumentation builds, libvame_count.so): every lane counts
 // the sub-block predictions it runs (the exact early exit skips the rest of
 // the algorithmic n_pred per sub-block); g_pred_count[kernel: quad, ctu], and
-// [2 + kernel]: those whose 9x9 window left the staged tile (clamped-global path).
+// [2 + 2 kernel + (3-CP pass)]: those whose 9x9 window left the staged tile
+// (the clamped-global path).
 #ifndef VAME_COUNT_PRED
 #define VAME_COUNT_PRED 0
 #endif
 #if VAME_COUNT_PRED
-__device__ unsigned long long g_pred_count[4];
+__device__ unsigned long long g_pred_count[6];
 #define PC_DECL unsigned pc_n = 0;
 #define PC_ADD pc_n++;
 #define PC_FLUSH { if (pc_n) atomicAdd(&g_pred_count[REGION == 128], (unsigned long long)pc_n); }
@@ -441,13 +453,127 @@ __device__ __forceinline__ void filter_rows(const unsigned* src, const uint4& KA
     __builtin_amdgcn_sched_barrier(0);
   }
 }
+// A wave some of whose windows leave the LDS tile: every lane runs the one
+// filter_rows computation, its window rows from the tile (in-tile lanes, taps
+// of their start parity) or from the frame (the others, re-aligned to an even
+// start, parity-0 taps), so such a wave computes its predictions once instead
+// of once per path.  The frame rows come in two batches (rows 0-3, rows 4-8,
+// each batch's loads in flight together): 6 dwords per row from the uniform
+// frame base, re-aligned by v_alignbit, or -- a window crossing the left /
+// right frame edge -- per-sample clamped loads; rows clamp to the frame
+// (clamp-to-edge, affine.cl:254-326).
+// One window row from the frame, as 5 dwords of sample pairs from an even
+// start: 6 dwords from the uniform frame base re-aligned by v_alignbit, or --
+// a window crossing the left / right frame edge -- per-sample clamped loads.
+__device__ __forceinline__ void frame_row(const uint16_t* __restrict__ ref, int wx, int y, int W,
+                                          bool wide, unsigned (&D)[5]) {
+  if (wide) {
+    const char* base = reinterpret_cast<const char*>(ref);
+    const unsigned a = (unsigned)wx * 2u, b = a & ~3u, sh = (a & 2u) << 3;  // sh: 0 or 16 bits
+    const unsigned off = (unsigned)y * (unsigned)W * 2u + b;
+    unsigned raw[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) raw[k] = *reinterpret_cast<const unsigned*>(base + (off + 4u * k));
+#pragma unroll
+    for (int q = 0; q < 5; q++) D[q] = __builtin_amdgcn_alignbit(raw[q + 1], raw[q], sh);
+  } else {
+    const uint16_t* row = ref + (size_t)y * W;
+#pragma unroll
+    for (int q = 0; q < 5; q++)
+      D[q] = (unsigned)row[clampi(wx + 2 * q, 0, W - 1)] | ((unsigned)row[clampi(wx + 2 * q + 1, 0, W - 1)] << 16);
+  }
+}
+// A wave some of whose windows leave the LDS tile: every lane runs the one
+// filter_rows computation, its window rows from the tile (in-tile lanes, taps
+// of their start parity) or from the frame (the others: rows clamped to the
+// frame, clamp-to-edge as affine.cl:254-326, re-aligned to an even start,
+// parity-0 taps), one row pair per step -- so such a wave computes its
+// predictions once, not once per path, and waits for 5 rounds of frame
+// loads instead of 9.
+template <int PITCH_DW>
+__device__ __forceinline__ void filter_rows_mixed(const unsigned* src, bool inTile,
+                                                  const uint16_t* __restrict__ ref, int wx, int wy, int W,
+                                                  int H, const uint4& KA, const uint4& KB, const uint4& G0,
+                                                  const uint4& G1, int (&acc)[4][4]) {
+  const bool wide = wx >= 0 && wx + 12 <= W;
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    unsigned E[2][5];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int row = 2 * k + h;
+      if (row < 9) {
+        if (inTile) {
+#pragma unroll
+          for (int q = 0; q < 5; q++) E[h][q] = src[row * PITCH_DW + q];
+        } else {
+          frame_row(ref, wx, clampi(wy + row, 0, H - 1), W, wide, E[h]);
+        }
+      }
+    }
+    int t0[4], t1[4] = {0, 0, 0, 0};
+    hrow_raw(E[0], KA, KB, t0);
+    if (k < 4) hrow_raw(E[1], KA, KB, t1);
+    vpair(k, t0, t1, G0, G1, acc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
 // Window leaves the LDS tile: clamp-to-edge loads from the frame
 // (affine.cl:254-326), one row at a time (a rare path, kept register-lean:
 // scalar vertical taps read from the LDS tap table).
+// Vertical taps of window row i into the output rows it feeds.
+__device__ __forceinline__ void vrow_acc(int i, const int (&t)[4], const unsigned* s_coef_dw, int fy,
+                                         int (&acc)[4][4]) {
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int m = i - r;  // vertical tap of window row i for output row r
+    if (m < 0 || m > 5) continue;
+    const unsigned pr = s_coef_dw[fy * 12 + (m >> 1)];  // set 0: (f0,f1) (f2,f3) (f4,f5)
+    const int cf = (int)(short)(m & 1 ? pr >> 16 : pr & 0xFFFF);
+#pragma unroll
+    for (int c = 0; c < 4; c++) acc[r][c] += t[c] * cf;
+  }
+}
+
+// The window read from the frame (it left the staged tile): rows clamped to
+// the frame.  A window whose samples wx .. wx + 11 lie inside its rows is
+// read as 6 dwords per row from the uniform frame base (32-bit offsets), the
+// loads of three rows in flight together, and re-aligned by v_alignbit; one
+// that crosses the left / right frame edge takes the per-sample clamped loads.
+// (The rows' latency dominates this path: 9 dependent round trips cost the
+// 2160p configs 10-20 % of their time.)
 __device__ __forceinline__ void filter_rows_global(const uint16_t* __restrict__ ref, int wx, int wy,
                                                    int W, int H, const uint4& KA, const uint4& KB,
                                                    const unsigned* s_coef_dw, int fy,
                                                    int (&acc)[4][4]) {
+  if (VAME_WIDE_GLOBAL && wx >= 0 && wx + 12 <= W) {
+    const char* base = reinterpret_cast<const char*>(ref);
+    const unsigned a = (unsigned)wx * 2u, b = a & ~3u, sh = (a & 2u) << 3;  // sh: 0 or 16 bits
+    constexpr int NB = VAME_GLOBAL_BATCH;  // rows whose loads are in flight together
+#pragma unroll 1
+    for (int i0 = 0; i0 < 9; i0 += NB) {
+      unsigned raw[NB][6];
+#pragma unroll
+      for (int j = 0; j < NB; j++) {
+        if (i0 + j >= 9) break;
+        const unsigned off = (unsigned)clampi(wy + i0 + j, 0, H - 1) * (unsigned)W * 2u + b;
+#pragma unroll
+        for (int k = 0; k < 6; k++) raw[j][k] = *reinterpret_cast<const unsigned*>(base + (off + 4u * k));
+      }
+#pragma unroll
+      for (int j = 0; j < NB; j++) {
+        if (i0 + j >= 9) break;
+        unsigned D[5];
+#pragma unroll
+        for (int q = 0; q < 5; q++) D[q] = __builtin_amdgcn_alignbit(raw[j][q + 1], raw[j][q], sh);
+        D[4] &= 0xFFFFu;  // sample wx + 9 meets a zero tap (as in the clamped path)
+        int t[4];
+        hrow(D, KA, KB, t);
+        vrow_acc(i0 + j, t, s_coef_dw, fy, acc);
+      }
+    }
+    return;
+  }
 #pragma unroll 1
   for (int i = 0; i < 9; i++) {
     const uint16_t* row = ref + (size_t)clampi(wy + i, 0, H - 1) * W;
@@ -460,15 +586,7 @@ __device__ __forceinline__ void filter_rows_global(const uint16_t* __restrict__ 
     }
     int t[4];
     hrow(D, KA, KB, t);
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int m = i - r;  // vertical tap of window row i for output row r
-      if (m < 0 || m > 5) continue;
-      const unsigned pr = s_coef_dw[fy * 12 + (m >> 1)];  // set 0: (f0,f1) (f2,f3) (f4,f5)
-      const int cf = (int)(short)(m & 1 ? pr >> 16 : pr & 0xFFFF);
-#pragma unroll
-      for (int c = 0; c < 4; c++) acc[r][c] += t[c] * cf;
-    }
+    vrow_acc(i, t, s_coef_dw, fy, acc);
   }
 }
 
@@ -584,7 +702,8 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
                                           const uint16_t* s_tile, int tx0, int ty0,
                                           const uint16_t* __restrict__ ref,
                                           const uint16_t* __restrict__ cur, int W, int H,
-                                          const uint4* s_coef, uint2 (&P)[4], uint2 (&O)[4]) {
+                                          const uint4* s_coef, uint2 (&P)[4], uint2 (&O)[4],
+                                          bool& outside) {
   {  // 32-bit byte offsets from the uniform frame base (frames < 4 GiB): the
      // saddr form of global_load, no 64-bit address arithmetic per row
     const unsigned b0 = (unsigned)((g.y + sy) * W + g.x + sx) * 2u, bw = (unsigned)W * 2u;
@@ -601,15 +720,13 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   clip_mv(mx, my, g.x, g.y, W, H);
   const int ix = mx >> 4, fx = mx & 15, iy = my >> 4, fy = my & 15;
   const int wx = g.x + sx + ix - 2, wy = g.y + sy + iy - 2;  // window origin (frame)
-  const int tx = wx - tx0, ty = wy - ty0;
-  const bool inTile = (unsigned)tx <= (unsigned)(TILE - 9) && (unsigned)ty <= (unsigned)(TILE - 9);
-#if VAME_COUNT_PRED
-  {  // instrumentation: windows outside the tile, one atomic per wave
-    const unsigned long long out = __builtin_amdgcn_ballot_w64(!inTile);
-    if (out && __lane_id() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
-      atomicAdd(&g_pred_count[2 + (TILE > 100)], (unsigned long long)__popcll(out));
+  int tx = wx - tx0, ty = wy - ty0;
+  if (VAME_ABLATE & 512) {  // timing-only: every window read from the tile (wrong results)
+    tx = clampi(tx, 0, TILE - 9);
+    ty = clampi(ty, 0, TILE - 9);
   }
-#endif
+  const bool inTile = (unsigned)tx <= (unsigned)(TILE - 9) && (unsigned)ty <= (unsigned)(TILE - 9);
+  outside = !inTile;
   if (!PROF && __builtin_amdgcn_ballot_w64(!(inTile && (fx | fy) == 0)) == 0) {
     // Every active lane has an integer MV inside the tile (e.g. every sub-block
     // of the first 2-CP prediction, from zero CPMVs): the phase-0 filter is the
@@ -631,7 +748,18 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   const uint4 KA = s_coef[fx * 3 + sp], KB = s_coef[fx * 3 + sp + 1];
   const uint4 G0 = s_coef[fy * 3 + 0], G1 = s_coef[fy * 3 + 1];
   int acc[4][4];
-  if (inTile) {
+  if (VAME_MIXED_FILTER && !PROF) {
+    // offsets folded into the rows (hrow_raw); the first tap pair overwrites acc (vpair)
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) acc[r][c] = 0;
+    const unsigned* src = reinterpret_cast<const unsigned*>(s_tile) + ((ty * TP + tx) >> 1);  // in-tile lanes
+    if (__builtin_amdgcn_ballot_w64(!inTile) == 0)
+      filter_rows<TP / 2>(src, KA, KB, G0, G1, acc);
+    else  // a wave with windows outside the tile: one filter pass for every lane
+      filter_rows_mixed<TP / 2>(src, inTile, ref, wx, wy, W, H, KA, KB, G0, G1, acc);
+  } else if (inTile) {
 #pragma unroll
     for (int r = 0; r < 4; r++)
 #pragma unroll
@@ -1529,14 +1657,23 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         int cp[6];
         for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
         const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
+        bool outside;
         const int satdLane = predict_sb<C::TILE, C::TP, PROF>(f, sxp, syp, gp, s_tile, tx0, ty0, ref, cur,
-                                                        W, H, s_coef, Pr, Og);
+                                                        W, H, s_coef, Pr, Og, outside);
+#if VAME_COUNT_PRED
+        {  // instrumentation: windows outside the tile, per kernel and pass, one atomic per wave
+          const unsigned long long out = __builtin_amdgcn_ballot_w64(outside);
+          if (out && __lane_id() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
+            atomicAdd(&g_pred_count[2 + 2 * (REGION == 128) + (ncp == 3)], (unsigned long long)__popcll(out));
+        }
+#endif
         if (kDup & 1) {
           MvField f2 = f;
           opaque(f2.bx);
           uint2 P2[4], O2[4];
+          bool out2;
           int s2 = predict_sb<C::TILE, C::TP, PROF>(f2, sxp, syp, gp, s_tile, tx0, ty0, ref, cur, W, H,
-                                              s_coef, P2, O2);
+                                              s_coef, P2, O2, out2);
           s2 += (int)(P2[0].x ^ P2[3].y ^ O2[1].x);
           asm volatile("" ::"v"(s2));
         }
