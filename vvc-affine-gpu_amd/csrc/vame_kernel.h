@@ -128,6 +128,9 @@ struct KParams {
 #ifndef VAME_MIXED_FILTER
 #define VAME_MIXED_FILTER 1
 #endif
+#ifndef VAME_MIXED_PIPE
+#define VAME_MIXED_PIPE 0
+#endif
 // Wave priority (s_setprio) during the latency-bound solve: its dependent
 // FP64 / LDS chain issues ahead of other waves' prediction work (~0.5 %;
 // priority 1 / 3 and priority over the whole post-prediction part measured
@@ -496,6 +499,13 @@ __device__ __forceinline__ void filter_rows_mixed(const unsigned* src, bool inTi
                                                   int H, const uint4& KA, const uint4& KB, const uint4& G0,
                                                   const uint4& G1, int (&acc)[4][4]) {
   const bool wide = wx >= 0 && wx + 12 <= W;
+#if VAME_MIXED_PIPE
+  unsigned Nx[2][5];  // the next row pair from the frame, loaded one step ahead
+  if (!inTile) {
+    frame_row(ref, wx, clampi(wy, 0, H - 1), W, wide, Nx[0]);
+    frame_row(ref, wx, clampi(wy + 1, 0, H - 1), W, wide, Nx[1]);
+  }
+#endif
 #pragma unroll
   for (int k = 0; k < 5; k++) {
     unsigned E[2][5];
@@ -507,10 +517,22 @@ __device__ __forceinline__ void filter_rows_mixed(const unsigned* src, bool inTi
 #pragma unroll
           for (int q = 0; q < 5; q++) E[h][q] = src[row * PITCH_DW + q];
         } else {
+#if VAME_MIXED_PIPE
+#pragma unroll
+          for (int q = 0; q < 5; q++) E[h][q] = Nx[h][q];
+#else
           frame_row(ref, wx, clampi(wy + row, 0, H - 1), W, wide, E[h]);
+#endif
         }
       }
     }
+#if VAME_MIXED_PIPE
+    if (!inTile && k < 4) {
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+        if (2 * k + 2 + h < 9) frame_row(ref, wx, clampi(wy + 2 * k + 2 + h, 0, H - 1), W, wide, Nx[h]);
+    }
+#endif
     int t0[4], t1[4] = {0, 0, 0, 0};
     hrow_raw(E[0], KA, KB, t0);
     if (k < 4) hrow_raw(E[1], KA, KB, t1);
