@@ -49,7 +49,7 @@ def main():
     frames = cfg["frames"] if n_pairs is None else frames_for_pairs(n_pairs)
     run = ShardRun(eng, cfg["W"], cfg["H"], qp, frames, cfg["modes"], args.gpus, args.rank_only, dev,
                    n_pairs=n_pairs)
-    cnt = (ctypes.c_ulonglong * 6)()
+    cnt = (ctypes.c_ulonglong * 12)()
     L.vame_debug_pred_count(cnt, 1)
     run.step()
     torch.cuda.synchronize()
@@ -63,7 +63,10 @@ def main():
            # executed predictions whose 9x9 window left the staged tile (clamped global loads)
            "outside_tile_frac_quad": (cnt[2] + cnt[3]) / max(cnt[0], 1),
            "outside_tile_frac_ctu": (cnt[4] + cnt[5]) / max(cnt[1], 1),
-           "outside_tile_quad_2cp_3cp": [cnt[2], cnt[3]], "outside_tile_ctu_2cp_3cp": [cnt[4], cnt[5]]}
+           "outside_tile_quad_2cp_3cp": [cnt[2], cnt[3]], "outside_tile_ctu_2cp_3cp": [cnt[4], cnt[5]],
+           # of the outside windows, those a margin wider by 4 / 8 / 16 px would hold
+           "outside_held_by_wider_margin_quad": [cnt[6], cnt[7], cnt[8]],
+           "outside_held_by_wider_margin_ctu": [cnt[9], cnt[10], cnt[11]]}
     print(json.dumps(out))
     eng.close()
 

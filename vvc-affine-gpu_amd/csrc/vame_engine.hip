@@ -638,13 +638,14 @@ int vame_debug_phase_cycles(unsigned long long* out32, int reset) {
 #if VAME_COUNT_PRED
 // instrumentation builds: sub-block predictions run, [quad, ctu], and those of
 // them whose window left the staged tile, [2 + quad 2-CP, quad 3-CP, ctu 2-CP,
-// ctu 3-CP] (see vame_kernel.h)
-int vame_debug_pred_count(unsigned long long* out6, int reset) {
-  if (!out6) return VAME_E_INVALID;
+// ctu 3-CP], and of those the ones a 4 / 8 / 16 px wider margin would hold,
+// [6 + quad x3, ctu x3] (see vame_kernel.h)
+int vame_debug_pred_count(unsigned long long* out12, int reset) {
+  if (!out12) return VAME_E_INVALID;
   VAME_HIP(hipDeviceSynchronize());
-  VAME_HIP(hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_pred_count), sizeof(unsigned long long) * 6));
+  VAME_HIP(hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_pred_count), sizeof(unsigned long long) * 12));
   if (reset) {
-    unsigned long long z[6] = {};
+    unsigned long long z[12] = {};
     VAME_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pred_count), z, sizeof(z)));
   }
   return VAME_OK;

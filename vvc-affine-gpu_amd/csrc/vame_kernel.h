@@ -131,6 +131,9 @@ struct KParams {
 #ifndef VAME_MIXED_PIPE
 #define VAME_MIXED_PIPE 0
 #endif
+#ifndef VAME_WIDE_X4
+#define VAME_WIDE_X4 1
+#endif
 // Wave priority (s_setprio) during the latency-bound solve: its dependent
 // FP64 / LDS chain issues ahead of other waves' prediction work (~0.5 %;
 // priority 1 / 3 and priority over the whole post-prediction part measured
@@ -146,7 +149,7 @@ constexpr int kSolvePrio = 3;
 #define VAME_COUNT_PRED 0
 #endif
 #if VAME_COUNT_PRED
-__device__ unsigned long long g_pred_count[6];
+__device__ unsigned long long g_pred_count[12];
 #define PC_DECL unsigned pc_n = 0;
 #define PC_ADD pc_n++;
 #define PC_FLUSH { if (pc_n) atomicAdd(&g_pred_count[REGION == 128], (unsigned long long)pc_n); }
@@ -475,8 +478,17 @@ __device__ __forceinline__ void frame_row(const uint16_t* __restrict__ ref, int 
     const unsigned a = (unsigned)wx * 2u, b = a & ~3u, sh = (a & 2u) << 3;  // sh: 0 or 16 bits
     const unsigned off = (unsigned)y * (unsigned)W * 2u + b;
     unsigned raw[6];
+#if VAME_WIDE_X4
+    // dword-aligned 16 + 8 byte loads (global_load_dwordx4 / x2 need only dword alignment)
+    typedef unsigned u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+    typedef unsigned u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+    const u32x4a4 v4 = *reinterpret_cast<const u32x4a4*>(base + off);
+    const u32x2a4 v2 = *reinterpret_cast<const u32x2a4*>(base + (off + 16u));
+    raw[0] = v4.x; raw[1] = v4.y; raw[2] = v4.z; raw[3] = v4.w; raw[4] = v2.x; raw[5] = v2.y;
+#else
 #pragma unroll
     for (int k = 0; k < 6; k++) raw[k] = *reinterpret_cast<const unsigned*>(base + (off + 4u * k));
+#endif
 #pragma unroll
     for (int q = 0; q < 5; q++) D[q] = __builtin_amdgcn_alignbit(raw[q + 1], raw[q], sh);
   } else {
@@ -749,6 +761,18 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   }
   const bool inTile = (unsigned)tx <= (unsigned)(TILE - 9) && (unsigned)ty <= (unsigned)(TILE - 9);
   outside = !inTile;
+#if VAME_COUNT_PRED
+  {  // instrumentation: outside windows that a 4 / 8 / 16 px wider margin would hold
+#pragma unroll
+    for (int e = 0; e < 3; e++) {
+      const int x = 4 << e;
+      const bool in = (unsigned)(tx + x) <= (unsigned)(TILE - 9 + 2 * x) && (unsigned)(ty + x) <= (unsigned)(TILE - 9 + 2 * x);
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(!inTile && in);
+      if (m && __lane_id() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
+        atomicAdd(&g_pred_count[6 + 3 * (TILE > 100) + e], (unsigned long long)__popcll(m));
+    }
+  }
+#endif
   if (!PROF && __builtin_amdgcn_ballot_w64(!(inTile && (fx | fy) == 0)) == 0) {
     // Every active lane has an integer MV inside the tile (e.g. every sub-block
     // of the first 2-CP prediction, from zero CPMVs): the phase-0 filter is the
