@@ -187,6 +187,9 @@ def test_parse_args_rejects_bad_input():
         distrun.parse_args(["-f", "2", "-s", "1000x1000", "-q", "32", "-o", "a", "-r", "b"])
     with pytest.raises(SystemExit):
         distrun.parse_args(["-f", "0", "-s", "416x240", "-q", "32", "-o", "a", "-r", "b"])
+    with pytest.raises(SystemExit):  # 3 pairs in 2 frames: at most 3 ranks
+        distrun.parse_args(["-f", "2", "-s", "416x240", "-q", "32", "-o", "a", "-r", "b", "--gpus", "4"])
+    assert distrun.parse_args(["-f", "2", "-s", "416x240", "-q", "32", "-o", "a", "-r", "b", "--gpus", "3"]).gpus == 3
 
 
 def test_world_size_must_match_gpus(tmp_path):

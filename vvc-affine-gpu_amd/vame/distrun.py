@@ -77,6 +77,9 @@ def parse_args(argv=None) -> argparse.Namespace:
         ap.error("frames and gpus must be >= 1, ExtraGradientIter in 0..64")
     if a.rank_only is not None and not 0 <= a.rank_only < a.gpus:
         ap.error("--rank-only K needs 0 <= K < --gpus")
+    if shard.sequence_pairs(a.frames) < a.gpus:  # every rank codes at least one pair
+        ap.error(f"--gpus {a.gpus} needs at least as many (POC, refIdx) pairs "
+                 f"({shard.sequence_pairs(a.frames)} in {a.frames} frames)")
     a.mode_mask = 3 if a.modes == "all" else 1
     return a
 
