@@ -190,7 +190,8 @@ long long vame_log_writer_refs(vame_log_writer* w, int poc, int ref0, int nrefs,
                                const int64_t* const* cost, const vame_cpmvs* const* cpmvs);
 int vame_log_writer_destroy(vame_log_writer* w);
 /* Deferred mode, for a frame-shard rank whose rows belong in the middle of
- * the files: after vame_log_writer_set_deferred(w, 1) the writer keeps each
+ * the files: after vame_log_writer_set_deferred(w, 1) (before its first POC;
+ * VAME_E_INVALID once rows were logged) the writer keeps each
  * file's rows in host memory instead of appending them.  Its files are
  * numbered 0 .. vame_log_writer_num_files - 1 (vame_log_writer_file_name);
  * vame_log_writer_sizes reports the bytes held per file, and

@@ -431,6 +431,8 @@ def test_log_writer_deferred_flush_at(tmp_path):
         for p, res in blk:
             logs.write_poc(pre, 416, 240, p, res, writer=w)
     writers[0].close()
+    with pytest.raises(logs.VameError):  # the mode is fixed once rows were logged
+        writers[1].defer()
     names = writers[1].files()
     assert names == logs.log_names(pre)
     base = [os.path.getsize(n) if os.path.exists(n) else 0 for n in names]

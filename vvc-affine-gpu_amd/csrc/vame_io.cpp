@@ -361,6 +361,7 @@ struct vame_log_writer {
   };
   static constexpr size_t kHeldBlock = size_t(32) << 20;
   bool deferred = false;
+  bool started = false;  // a POC was logged (the mode is fixed from then on)
   std::vector<Held> held;
   ~vame_log_writer() {
     for (int fd : fds)
@@ -430,6 +431,7 @@ long long vame_log_writer_refs(vame_log_writer* w, int poc, int ref0, int nrefs,
         for (int c = 0; c < nchunks; c++) tasks.push_back({r, m, g, c});
     }
   if (w->bufs.size() < tasks.size()) w->bufs.resize(tasks.size());
+  w->started = true;
   w->pool->run((int)tasks.size(), [&](int i) {
     const Task& t = tasks[i];
     format_rows(w->bufs[i], t.m >> 1, t.g, t.c * kLogChunk, std::min(w->nCtus, (t.c + 1) * kLogChunk),
@@ -513,7 +515,7 @@ long long vame_log_writer_refs(vame_log_writer* w, int poc, int ref0, int nrefs,
 }
 
 int vame_log_writer_set_deferred(vame_log_writer* w, int deferred) {
-  if (!w) return VAME_E_INVALID;
+  if (!w || w->started) return VAME_E_INVALID;  // rows already appended or held
   w->deferred = deferred != 0;
   w->held.resize(w->paths.size());
   return VAME_OK;
