@@ -106,14 +106,16 @@ struct KParams {
 // bit 1 skip the gradient math, bit 2 skip the reductions of the equations,
 // bit 3 skip the prediction math, bit 4 skip the 128-class launch, bit 5 skip
 // the quadrant launch, bit 8 (host) 128-class templates without the 128x64 /
-// 64x128 items, bit 9 every 9x9 window read from the tile (no clamped-global path).
+// 64x128 items, bit 9 every 9x9 window read from the tile (no clamped-global path),
+// bit 10 the same in the 3-CP pass only.
 #ifndef VAME_ABLATE
 #define VAME_ABLATE 0
 #endif
 // VAME_DUP (timing-only builds, results stay correct): run a phase twice to
 // price it in throughput terms: bit 0 prediction, bit 1 gradient, bit 2
 // equation reduction, bit 6 the tile staging round trip, bit 4 the solve (on the system itself, before the real
-// one rebuilds it: no extra LDS); with bit 5 set, only in the 3-CP pass.
+// one rebuilds it: no extra LDS); with bit 5 set, only in the 3-CP pass; bit 7
+// adds a workgroup barrier between the 2-CP and 3-CP passes of autonomous items.
 #ifndef VAME_DUP
 #define VAME_DUP 0
 #endif
@@ -731,7 +733,7 @@ __device__ __forceinline__ void prof_refine(const int (&acc)[4][4], const MvFiel
 // :1096-1239, PROF off), SATD against the original (aux_functions.cl:1940-2043).
 // The prediction stays in registers (P[r] = packed sample pairs of row r) for
 // the gradient step, and so do the original samples (O[r]).
-template <int TILE, int TP, bool PROF>
+template <int TILE, int TP, bool PROF, bool FORCE_TILE = false>
 __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, const Geo& g,
                                           const uint16_t* s_tile, int tx0, int ty0,
                                           const uint16_t* __restrict__ ref,
@@ -755,7 +757,7 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   const int ix = mx >> 4, fx = mx & 15, iy = my >> 4, fy = my & 15;
   const int wx = g.x + sx + ix - 2, wy = g.y + sy + iy - 2;  // window origin (frame)
   int tx = wx - tx0, ty = wy - ty0;
-  if (VAME_ABLATE & 512) {  // timing-only: every window read from the tile (wrong results)
+  if ((VAME_ABLATE & 512) || FORCE_TILE) {  // timing-only: every window read from the tile (wrong results)
     tx = clampi(tx, 0, TILE - 9);
     ty = clampi(ty, 0, TILE - 9);
   }
@@ -1704,8 +1706,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
         const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
         bool outside;
-        const int satdLane = predict_sb<C::TILE, C::TP, PROF>(f, sxp, syp, gp, s_tile, tx0, ty0, ref, cur,
-                                                        W, H, s_coef, Pr, Og, outside);
+        const int satdLane = predict_sb<C::TILE, C::TP, PROF, (VAME_ABLATE & 1024) != 0 && ncp == 3>(
+            f, sxp, syp, gp, s_tile, tx0, ty0, ref, cur, W, H, s_coef, Pr, Og, outside);
 #if VAME_COUNT_PRED
         {  // instrumentation: windows outside the tile, per kernel and pass, one atomic per wave
           const unsigned long long out = __builtin_amdgcn_ballot_w64(outside);
@@ -1959,6 +1961,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     if constexpr (run3) run_pass(I3{}, T{}, F{});
   } else {
     if constexpr (run2) run_pass(I2{}, F{}, KeepS{});
+    if constexpr (run2 && run3 && (VAME_DUP & 128) != 0) {  // timing-only: a barrier between the passes
+      __syncthreads();
+    }
     if constexpr (run3) run_pass(I3{}, F{}, F{});
   }
   PH_FLUSH
