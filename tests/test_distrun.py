@@ -242,3 +242,75 @@ def test_distrun_two_ranks_equals_cli(tmp_path, W, H, n):
         out, stdout = run_distrun_gpu(tmp_path, W, H, n, 32, name, ("--gpus", "2", *extra))
         assert len(compare_dirs(out, cli)) == 40, name
         assert "LOG_BYTES," in stdout and '"ranks": 2' in stdout
+
+
+class FakeEngine:
+    """Deterministic stand-in results (not the algorithm, but its record shape:
+    costs below 2^31, LB = 0 for 2 CP): every record a hash of the (cur, ref,
+    lambda) triple it was computed for, so a run's logs depend on
+    exactly which frames each pair used -- enough to test the shard, ingest and
+    log-placement plumbing at many ranks without the oracle's cost."""
+
+    def __init__(self, W, H):
+        self.n_ctus = O.lib().vame_oracle_num_ctus(W, H)
+
+    def n_cus(self, align):
+        return self.n_ctus * (284 if align else 201)
+
+    def alloc_poc(self, nrefs, modes=3):
+        return LookupEngine.alloc_poc(self, nrefs, modes)
+
+    def affine_me_batch(self, jobs, modes, extra):
+        for cur, refs, lam, out in jobs:
+            for r, ref in enumerate(refs):
+                h = digest(cur.numpy().view(np.uint16)) + digest(ref.numpy().view(np.uint16)) + repr(lam)
+                seed = int(hashlib.sha1(h.encode()).hexdigest()[:8], 16)
+                g = torch.Generator().manual_seed(seed)
+                for (r2, m), (c, p) in out.items():
+                    if r2 == r:
+                        c.copy_(torch.randint(0, 1 << 20, c.shape, generator=g))
+                        p.copy_(torch.randint(-4096, 4096, p.shape, generator=g, dtype=torch.int32))
+                        p[:, 0] = 3 if m.endswith("3CP") else 2
+                        if m.endswith("2CP"):  # 2-CP records carry LB = (0, 0) (SURVEY T11)
+                            p[:, 5:] = 0
+        return [j[3] for j in jobs]
+
+
+def fake_worker(rank, world, port, argv):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a = distrun.parse_args(argv)
+    distrun.run_rank(a, world, rank, FakeEngine(a.W, a.H), torch.device("cpu"), dist)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_eight_ranks_cut_pocs_and_long_term_refs(tmp_path):
+    """8 ranks over 40 frames (150 pairs): POCs 7, 16, 21, 26, 31 cut
+    between ranks, long-term references of POC 8 / 16 / 24 / 32 in play, every
+    rank's frames read through the shared CSV line index; both log paths equal
+    a one-rank run byte for byte (the plumbing of BASELINE configs[4] at N = 8;
+    stand-in results, the HIP path's parity is covered elsewhere)."""
+    n = 40
+    orig, recon = synth_sequence(416, 240, n, 32, seed=5)
+    write_csv(str(tmp_path / "orig.csv"), orig)
+    write_csv(str(tmp_path / "recon.csv"), recon)
+    owners = {}
+    for r in range(8):
+        for p, _ in shard.pair_shard(n, 8, r):
+            owners.setdefault(p, []).append(r)
+    assert [p for p, o in owners.items() if len(o) > 1] == [7, 16, 21, 26, 31]
+
+    def argv(out, *extra):
+        out.mkdir()
+        return ["-f", str(n), "-s", "416x240", "-q", "32", "-o", str(tmp_path / "orig.csv"),
+                "-r", str(tmp_path / "recon.csv"), "-l", str(out / "log"), "--modes", "2cp", *extra]
+    one = tmp_path / "one"
+    a = distrun.parse_args(argv(one))
+    distrun.run_rank(a, 1, 0, FakeEngine(416, 240), torch.device("cpu"))
+    from vame.launch import free_port
+    for name, extra in (("gather8", ()), ("shard8", ("--shard-logs",))):
+        mp.spawn(fake_worker, args=(8, free_port(), argv(tmp_path / name, *extra)), nprocs=8, join=True)
+        assert len(compare_dirs(tmp_path / name, one)) == 20, name

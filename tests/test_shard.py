@@ -341,3 +341,23 @@ def test_rank_only_block_and_verify_own():
     run.step()
     chk = run.verify_own()
     assert chk["byte_identical"] and [p for p, _, _ in chk["pocs"]] == [4, 5]
+
+
+def test_pack_refuses_records_outside_the_compact_form():
+    """The compact records drop 2-CP LB and the cost's upper half: pack refuses
+    results that would not survive that (the kernels never produce them)."""
+    n = 6
+    cost = torch.zeros(n, dtype=torch.int64)
+    cp = torch.zeros((n, 7), dtype=torch.int32)
+    cp[:, 0] = 2
+    shard.pack([{(0, "FULL_2CP"): (cost, cp)}])
+    bad_lb = cp.clone()
+    bad_lb[3, 5] = 1
+    with pytest.raises(ValueError):
+        shard.pack([{(0, "FULL_2CP"): (cost, bad_lb)}])
+    with pytest.raises(ValueError):
+        shard.pack([{(0, "FULL_2CP"): (cost + 2**31, cp)}])
+    cp3 = cp.clone()
+    cp3[:, 0] = 3
+    cp3[:, 5:] = 7  # 3-CP records keep LB
+    shard.pack([{(0, "FULL_3CP"): (cost, cp3)}])

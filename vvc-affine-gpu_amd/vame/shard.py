@@ -115,11 +115,13 @@ def ncp_of(mode: str) -> int:
     return 3 if mode.endswith("3CP") else 2
 
 
-def pack(results: list[dict], words: int | None = None, device=None, modes: int | None = None) -> torch.Tensor:
+def pack(results: list[dict], words: int | None = None, device=None, modes: int | None = None,
+         validate: bool = True) -> torch.Tensor:
     """Concatenate the results of several POCs ({(ref, MODE): (cost int64[n],
     cpmv int32[n, 7])}, in POC order) into one int32 slab of compact records,
     zero padded to `words`.  With `modes`, every POC must hold exactly the
-    keys `unpack` will expect for that mode mask."""
+    keys `unpack` will expect for that mode mask; with `validate`, every record
+    must fit the compact form (0 <= cost < 2^31, 2-CP LB = (0, 0))."""
     parts = []
     for res in results:
         if modes is not None:
@@ -128,6 +130,11 @@ def pack(results: list[dict], words: int | None = None, device=None, modes: int 
                 raise ValueError(f"results {sorted(res)} do not match mode mask {modes}")
         for key in sorted(res, key=lambda k: (k[0], MODES.index(k[1]))):
             cost, cpmv = res[key]
+            if validate:  # the compact form drops 2-CP LB and the cost's upper half
+                cp7 = cpmv.reshape(-1, 7)
+                if bool((cost < 0).any() or (cost >= 2**31).any()) or (
+                        ncp_of(key[1]) == 2 and bool(cp7[:, 5:].any())):
+                    raise ValueError(f"records of {key} do not fit the compact form")
             parts.append(cost.reshape(-1).to(torch.int32))
             parts.append(cpmv.reshape(-1, 7)[:, 1:1 + 2 * ncp_of(key[1])].reshape(-1).to(torch.int32))
     flat = torch.cat(parts) if parts else torch.empty(0, dtype=torch.int32, device=device)
