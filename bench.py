@@ -65,6 +65,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--prewarm-s", type=float, default=0.25,
+                    help="untimed steps until this much wall time has passed, before the warmup "
+                         "steps (GPU clocks settle; 0 = none)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--qp", type=int, default=None)
     ap.add_argument("--frames", type=int, default=None,
@@ -140,6 +143,13 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
+    # clocks settle before the warmup steps: a short driver run (--steps 20,
+    # about 20 ms of GPU work at c2) would otherwise time a GPU still ramping up
+    prewarm_steps, t_pw = 0, time.perf_counter()
+    while time.perf_counter() - t_pw < args.prewarm_s:
+        run.step()
+        torch.cuda.synchronize()
+        prewarm_steps += 1
     for _ in range(args.warmup):
         run.step()
     barrier()
@@ -208,6 +218,7 @@ def main():
         "n_gpus": 1 if args.rank_only is not None else world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "prewarm": {"seconds": args.prewarm_s, "steps": prewarm_steps},
         "ms_per_step": tmax * 1e3 / args.steps,
         # rank 0's per-step GPU times (HIP events at the step boundaries)
         "step_ms": {"median": step_ms[len(step_ms) // 2], "min": step_ms[0], "max": step_ms[-1]},

@@ -49,6 +49,8 @@ struct vame_ctx {
   bool timing = false;
   // PROF on (vame_set_prof): the *_prof kernels
   bool prof = false;
+  // VAME_JOIN_EACH=1: join the two streams after every launch of a batch
+  bool joinEach = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];
   size_t evUsed[2] = {0, 0};
 };
@@ -333,7 +335,7 @@ KernelFn kernel_for(bool prof, int mode) {
   }
 }
 
-int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
+int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool quadHalf, bool bigItems,
            hipStream_t stream) {
   // 128-class items (big LDS, 1 workgroup per CU) and quadrant items run on
   // two streams so they overlap: the 128-class kernel on the caller's stream,
@@ -341,10 +343,15 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
   // workgroup needs a whole CU (16 waves, 81 KB LDS): issued first, its
   // workgroups take CUs before the quadrant ones fill them, and the small
   // quadrant workgroups, not the long 128-class ones, make the tail
-  // (batched c2 step 1.32 -> 1.245 ms).
+  // (batched c2 step 1.32 -> 1.245 ms).  The launches of one batch (32 pairs
+  // each) fork once and join once: launch k + 1's kernels follow launch k's on
+  // their own streams, so the 128-class workgroups left at the end of a
+  // launch share the GPU with the next launch's quadrant kernel instead of
+  // draining it alone.
   if (VAME_ABLATE & 16) bigItems = false;  // timing-only builds
   if (VAME_ABLATE & 32) quadFull = quadHalf = false;
-  const int mode = (kp.run2 ? 1 : 0) | (kp.run3 ? 2 : 0);  // the kernel instance (MODE)
+  if (kps.empty()) return VAME_OK;
+  const int mode = (kps[0].run2 ? 1 : 0) | (kps[0].run3 ? 2 : 0);  // the kernel instance (MODE)
   if (mode == 0) return VAME_OK;
   const bool fork = bigItems && (quadFull || quadHalf);
   hipStream_t sBig = stream, sQuad = stream;
@@ -353,7 +360,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
     sQuad = c->side;
   }
-  auto big = [&]() -> int {
+  auto big = [&](const KParams& kp) -> int {
     KParams kb = kp;
     kb.items = c->dBig;
     kb.nItems = c->nBig;
@@ -365,7 +372,7 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     VAME_TRY(time_end(c, 1, sBig));
     return VAME_OK;
   };
-  auto quad = [&]() -> int {
+  auto quad = [&](const KParams& kp) -> int {
     KParams kq = kp;
     kq.items = quadFull ? c->dQuad : c->dQuad + c->nQuadFull;
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
@@ -377,11 +384,17 @@ int launch(vame_ctx* c, KParams kp, bool quadFull, bool quadHalf, bool bigItems,
     VAME_TRY(time_end(c, 0, sQuad));
     return VAME_OK;
   };
-  if (bigItems) VAME_TRY(big());
-  if (quadFull || quadHalf) VAME_TRY(quad());
-  if (fork) {
-    VAME_HIP(hipEventRecord(c->evJoin, c->side));
-    VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
+  for (size_t k = 0; k < kps.size(); k++) {
+    if (bigItems) VAME_TRY(big(kps[k]));
+    if (quadFull || quadHalf) VAME_TRY(quad(kps[k]));
+    if (fork && (c->joinEach || k + 1 == kps.size())) {
+      VAME_HIP(hipEventRecord(c->evJoin, c->side));
+      VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
+      if (k + 1 < kps.size()) {  // VAME_JOIN_EACH: fork again for the next launch
+        VAME_HIP(hipEventRecord(c->evFork, stream));
+        VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
+      }
+    }
   }
   return VAME_OK;
 }
@@ -449,6 +462,7 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   hipError_t e = hipMalloc(&c->dQuad, quad.size() * sizeof(Item));
   // tuning knobs of the block order (defaults measured on MI355X)
   const int xcdOrder = env_int("VAME_XCD_ORDER", 0);
+  c->joinEach = env_int("VAME_JOIN_EACH", 0) != 0;
   c->groupCombos[0] = std::max(8, env_int("VAME_GROUP_COMBOS", 408));
   c->groupCombos[1] = std::max(8, env_int("VAME_GROUP_COMBOS_BIG", c->groupCombos[0]));
   for (int k = 0; k < 2 && e == hipSuccess; k++) {
@@ -513,7 +527,7 @@ int vame_affine_me(vame_ctx* c, const uint16_t* ref, const uint16_t* cur, float 
   kp.pair[0].cost[mode] = cost;
   kp.pair[0].cpmv[mode] = reinterpret_cast<vame_cpmvs_dev*>(cpmvs);
   kp.prev[align] = reinterpret_cast<const vame_cpmvs_dev*>(prev);
-  return launch(c, kp, align == 0, align == 1, align == 0, (hipStream_t)stream);
+  return launch(c, std::vector<KParams>{kp}, align == 0, align == 1, align == 0, (hipStream_t)stream);
 }
 
 int vame_pred_mask(int mode_mask) {
@@ -545,6 +559,7 @@ int vame_affine_me_batch(vame_ctx* c, const vame_poc_job* jobs, int njobs, int m
   DeviceGuard guard(c->device);
   VAME_HIP(guard.err);
   // every (POC, refIdx) pair of the batch, kMaxPairs per launch
+  std::vector<KParams> kps;
   KParams kp;
   memset(&kp, 0, sizeof(kp));
   fill_common(kp, c, extra);
@@ -563,12 +578,12 @@ int vame_affine_me_batch(vame_ctx* c, const vame_poc_job* jobs, int njobs, int m
       }
       const bool last = j == njobs - 1 && r == jb.nrefs - 1;
       if (kp.nPairs == kMaxPairs || last) {
-        VAME_TRY(launch(c, kp, doFull, doHalf, doFull, (hipStream_t)stream));
+        kps.push_back(kp);
         kp.nPairs = 0;
       }
     }
   }
-  return VAME_OK;
+  return launch(c, kps, doFull, doHalf, doFull, (hipStream_t)stream);
 }
 
 int vame_affine_me_poc(vame_ctx* c, const uint16_t* cur, const uint16_t* const* refs, int nrefs,
