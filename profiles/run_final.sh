@@ -7,3 +7,5 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.log
 timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
 tail -c 400 $O/bench_default.json
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_s20.json 2> $O/bench_s20.err || { tail -20 $O/bench_s20.err; exit 1; }
+tail -c 300 $O/bench_s20.json
