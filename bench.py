@@ -241,6 +241,10 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": prof.get("traffic"),
                      "kernel": "affine_me_quad",
                      "avg_launch_ms": quad_ms / max(quad_n, 1),
+                     "launches": quad_n,
+                     # the same kernel's average under rocprofv3 over the timed
+                     # dispatches of a traced run of this config (profiles/)
+                     "rocprof_avg_ms": prof.get("rocprof_avg_ms"),
                      "alg_bytes_per_launch": quad_bytes / max(quad_n, 1),
                      # fraction of the algorithmic sub-block predictions the exact
                      # early exit actually runs (instrumented build, profiles/)
@@ -249,6 +253,7 @@ def main():
                      "valu": prof.get("valu"),
                      "affine_me_ctu": {"achieved": big_achieved, "frac": big_achieved / HBM_PEAK_GBS,
                                        "avg_launch_ms": big_ms / max(big_n, 1),
+                                       "launches": big_n,
                                        "alg_bytes_per_launch": big_bytes / max(big_n, 1)},
                      "fused_poc_launch": {"achieved": span_achieved,
                                           "frac": span_achieved / HBM_PEAK_GBS,
@@ -289,7 +294,8 @@ def load_profile(config: str, avg_launch_ms: float) -> dict:
         return {}
     p = json.load(open(path))
     out = {"traffic": p.get("quad_hbm_bytes_per_launch"),
-           "executed_pred_frac": p.get("executed_pred_frac")}
+           "executed_pred_frac": p.get("executed_pred_frac"),
+           "rocprof_avg_ms": p.get("quad_timed_avg_ms_rocprof")}
     sq = p.get("quad_sq")
     if sq and avg_launch_ms > 0:
         clk = sq["clock_ghz"]

@@ -4,7 +4,9 @@
     python profiles/pmc_summary.py <prof_dir> <out.json>
 
 Reads, under <prof_dir>:
-  trace/run_kernel_stats.csv      rocprofv3 --kernel-trace --stats (durations)
+  trace/run_kernel_stats.csv      rocprofv3 --kernel-trace --stats (durations, all dispatches)
+  trace/run_kernel_trace.csv      the same run's dispatches: the timed steps' average,
+  trace.log                       located with the traced run's own bench line
   pmc_fetch/, pmc_write/          one PMC pass each: FETCH_SIZE, WRITE_SIZE
   pmc_sq/                         one PMC pass: SQ_WAVES SQ_INSTS_VALU
                                   SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES ... GRBM_GUI_ACTIVE
@@ -60,6 +62,43 @@ def mean(v):
     return sum(v) / len(v) if v else None
 
 
+def timed_dispatches(d):
+    """{kernel: [duration ms of each dispatch of the traced run's timed steps]}.
+    The traced run's own bench line (trace.log) gives prewarm P, warmup W,
+    steps K and the kernel's launches L in the K timed steps; its dispatches,
+    in order, are the P + W untimed steps' (L / K each), the timed ones, then
+    any after the timed region.  Also returns that line's event averages."""
+    line = None
+    log = os.path.join(d, "trace.log")
+    if os.path.exists(log):
+        for l in open(log):
+            if l.startswith("{"):
+                line = json.loads(l)
+    path = os.path.join(d, "trace", "run_kernel_trace.csv")
+    if line is None or not os.path.exists(path):
+        return {}, {}
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    per = defaultdict(list)
+    for r in rows:
+        per[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    K, W = line["steps"], line["warmup"]
+    P = (line.get("prewarm") or {}).get("steps", 0)
+    roof = line["roofline"]
+    launches = {"affine_me_quad": roof.get("launches"),
+                "affine_me_ctu": roof.get("affine_me_ctu", {}).get("launches")}
+    events = {"affine_me_quad": roof.get("avg_launch_ms"),
+              "affine_me_ctu": roof.get("affine_me_ctu", {}).get("avg_launch_ms")}
+    out = {}
+    for k, L in launches.items():
+        if not L or L % K or k not in per:
+            continue
+        lo = (P + W) * (L // K)
+        if len(per[k]) < lo + L:
+            continue
+        out[k] = per[k][lo:lo + L]
+    return out, events
+
+
 def main():
     d, out = sys.argv[1], sys.argv[2]
     stats = {}
@@ -100,7 +139,14 @@ def main():
                                           ("wait_inst_any", "SQ_WAIT_INST_ANY"),
                                           ("wait_any", "SQ_WAIT_ANY")) if c in sqm}
         res["kernels"][k] = e
+    timed, events = timed_dispatches(d)
+    for k, v in timed.items():
+        e = res["kernels"].setdefault(k, {})
+        e["timed_dispatches"] = len(v)
+        e["timed_avg_ms"] = mean(v)
+        e["traced_run_event_avg_ms"] = events.get(k)
     q = res["kernels"].get("affine_me_quad", {})
+    res["quad_timed_avg_ms_rocprof"] = q.get("timed_avg_ms")
     res["quad_hbm_bytes_per_launch"] = q.get("hbm_bytes_per_launch")
     res["quad_avg_ms_rocprof"] = q.get("avg_ms")
     if "sq_per_launch" in q:
