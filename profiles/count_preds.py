@@ -49,7 +49,7 @@ def main():
     frames = cfg["frames"] if n_pairs is None else frames_for_pairs(n_pairs)
     run = ShardRun(eng, cfg["W"], cfg["H"], qp, frames, cfg["modes"], args.gpus, args.rank_only, dev,
                    n_pairs=n_pairs)
-    cnt = (ctypes.c_ulonglong * 12)()
+    cnt = (ctypes.c_ulonglong * 20)()
     L.vame_debug_pred_count(cnt, 1)
     run.step()
     torch.cuda.synchronize()
@@ -66,7 +66,13 @@ def main():
            "outside_tile_quad_2cp_3cp": [cnt[2], cnt[3]], "outside_tile_ctu_2cp_3cp": [cnt[4], cnt[5]],
            # of the outside windows, those a margin wider by 4 / 8 / 16 px would hold
            "outside_held_by_wider_margin_quad": [cnt[6], cnt[7], cnt[8]],
-           "outside_held_by_wider_margin_ctu": [cnt[9], cnt[10], cnt[11]]}
+           "outside_held_by_wider_margin_ctu": [cnt[9], cnt[10], cnt[11]],
+           # lane use of the prediction steps: predictions run / 64 lane slots of
+           # the waves that ran the step; and the same over the waves holding
+           # several CUs (lanes of settled CUs idle while the wave iterates)
+           "lane_use_quad": cnt[0] / max(cnt[12], 1), "lane_use_ctu": cnt[1] / max(cnt[13], 1),
+           "multi_cu_wave_slots_frac_quad": cnt[14] / max(cnt[12], 1),
+           "multi_cu_wave_lane_use_quad": cnt[16] / max(cnt[14], 1)}
     print(json.dumps(out))
     eng.close()
 

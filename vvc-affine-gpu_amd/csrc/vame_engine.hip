@@ -654,13 +654,14 @@ int vame_debug_phase_cycles(unsigned long long* out32, int reset) {
 // instrumentation builds: sub-block predictions run, [quad, ctu], and those of
 // them whose window left the staged tile, [2 + quad 2-CP, quad 3-CP, ctu 2-CP,
 // ctu 3-CP], and of those the ones a 4 / 8 / 16 px wider margin would hold,
-// [6 + quad x3, ctu x3] (see vame_kernel.h)
-int vame_debug_pred_count(unsigned long long* out12, int reset) {
-  if (!out12) return VAME_E_INVALID;
+// [6 + quad x3, ctu x3], then the wave lane slots [12 + kernel], [14 + kernel],
+// [16 + kernel] (see vame_kernel.h)
+int vame_debug_pred_count(unsigned long long* out20, int reset) {
+  if (!out20) return VAME_E_INVALID;
   VAME_HIP(hipDeviceSynchronize());
-  VAME_HIP(hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_pred_count), sizeof(unsigned long long) * 12));
+  VAME_HIP(hipMemcpyFromSymbol(out20, HIP_SYMBOL(g_pred_count), sizeof(unsigned long long) * 20));
   if (reset) {
-    unsigned long long z[12] = {};
+    unsigned long long z[20] = {};
     VAME_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pred_count), z, sizeof(z)));
   }
   return VAME_OK;

@@ -146,15 +146,35 @@ constexpr int kSolvePrio = 3;
 // the sub-block predictions it runs (the exact early exit skips the rest of
 // the algorithmic n_pred per sub-block); g_pred_count[kernel: quad, ctu], and
 // [2 + 2 kernel + (3-CP pass)]: those whose 9x9 window left the staged tile
-// (the clamped-global path).
+// (the clamped-global path); [12 + kernel]: 64 lane slots per wave that runs a
+// prediction step, [14 + kernel] / [16 + kernel]: the same slots and the
+// predictions run, of waves holding several CUs (autonomous, < 64 sub-blocks
+// per CU) -- the lanes an iteration spends on settled CUs.
 #ifndef VAME_COUNT_PRED
 #define VAME_COUNT_PRED 0
 #endif
 #if VAME_COUNT_PRED
-__device__ unsigned long long g_pred_count[12];
-#define PC_DECL unsigned pc_n = 0;
-#define PC_ADD pc_n++;
-#define PC_FLUSH { if (pc_n) atomicAdd(&g_pred_count[REGION == 128], (unsigned long long)pc_n); }
+__device__ unsigned long long g_pred_count[20];
+#define PC_DECL unsigned pc_n = 0, pc_w = 0, pc_mw = 0, pc_me = 0;
+#define PC_ADD                                                           \
+  {                                                                      \
+    pc_n++;                                                              \
+    const unsigned long long m_ = __builtin_amdgcn_ballot_w64(true);     \
+    if (__lane_id() == __builtin_ctzll(m_)) {                            \
+      pc_w += 64;                                                        \
+      if (!coop && logS < 6) {                                           \
+        pc_mw += 64;                                                     \
+        pc_me += __popcll(m_);                                           \
+      }                                                                  \
+    }                                                                    \
+  }
+#define PC_FLUSH                                                                                \
+  {                                                                                             \
+    if (pc_n) atomicAdd(&g_pred_count[REGION == 128], (unsigned long long)pc_n);               \
+    if (pc_w) atomicAdd(&g_pred_count[12 + (REGION == 128)], (unsigned long long)pc_w);        \
+    if (pc_mw) atomicAdd(&g_pred_count[14 + (REGION == 128)], (unsigned long long)pc_mw);      \
+    if (pc_me) atomicAdd(&g_pred_count[16 + (REGION == 128)], (unsigned long long)pc_me);      \
+  }
 #else
 #define PC_DECL
 #define PC_ADD
