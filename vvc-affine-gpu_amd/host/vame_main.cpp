@@ -46,6 +46,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -343,50 +344,122 @@ void fail(Shared* S, const std::string& msg) {
   S->cv.notify_all();
 }
 
-// One device: uploads the frames its POCs need, runs them in order on one
-// stream, and hands each POC's results (pinned host slab) to the writer.
+// One device: runs its POCs in order on one stream, uploading each batch's
+// frames on a second stream while the previous batch computes, and hands each
+// POC's results (pinned host slab) to the writer.
 void gpu_worker(Job J) {
   Shared* S = J.S;
+  // VAME_CLI_TRACE=1: the worker's timeline on stderr (host and GPU)
+  const bool trace = getenv("VAME_CLI_TRACE") && atoi(getenv("VAME_CLI_TRACE")) != 0;
+  const double w0 = now_s();
   GPU_CHECK(hipSetDevice(J.device), "hipSetDevice");
   vame_ctx* ctx = nullptr;
   VAME_CHECK(vame_create(&ctx, J.device, J.W, J.H), "vame_create");
+  const double w1 = now_s();
   VAME_CHECK(vame_set_prof(ctx, J.prof ? 1 : 0), "vame_set_prof");
-  hipStream_t st;
+  hipStream_t st, up, dn;  // compute; frame uploads; result downloads
   GPU_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+  GPU_CHECK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking), "hipStreamCreate");
+  GPU_CHECK(hipStreamCreateWithFlags(&dn, hipStreamNonBlocking), "hipStreamCreate");
   const size_t fsz = (size_t)J.W * J.H;
-  // frames: orig of each POC, recon of every label its ring holds
+  // frames: orig of each POC, recon of every label its ring holds -- allocated
+  // here in two blocks, uploaded per batch (upload_frames below)
   std::map<int, uint16_t*> dorig, drecon;
-  for (int p : J.pocs) {
-    GPU_CHECK(hipMalloc(&dorig[p], fsz * 2), "hipMalloc frame");
-    GPU_CHECK(hipMemcpyAsync(dorig[p], J.orig + (size_t)(p - 1) * fsz, fsz * 2,
-                             hipMemcpyHostToDevice, st),
-              "upload orig");
-    int refs[4];
-    const int n = vame_ref_list(p, refs);
-    for (int r = 0; r < n; r++)
-      if (!drecon.count(refs[r])) {
-        GPU_CHECK(hipMalloc(&drecon[refs[r]], fsz * 2), "hipMalloc frame");
-        GPU_CHECK(hipMemcpyAsync(drecon[refs[r]], J.recon + (size_t)refs[r] * fsz, fsz * 2,
-                                 hipMemcpyHostToDevice, st),
-                  "upload recon");
-      }
+  uint16_t *origBlk = nullptr, *reconBlk = nullptr;
+  {
+    std::vector<int> labels;
+    for (int p : J.pocs) {
+      int refs[4];
+      const int n = vame_ref_list(p, refs);
+      for (int r = 0; r < n; r++)
+        if (std::find(labels.begin(), labels.end(), refs[r]) == labels.end()) labels.push_back(refs[r]);
+    }
+    GPU_CHECK(hipMalloc(&origBlk, J.pocs.size() * fsz * 2), "hipMalloc frames");
+    GPU_CHECK(hipMalloc(&reconBlk, labels.size() * fsz * 2), "hipMalloc frames");
+    for (size_t i = 0; i < J.pocs.size(); i++) dorig[J.pocs[i]] = origBlk + i * fsz;
+    for (size_t i = 0; i < labels.size(); i++) drecon[labels[i]] = reconBlk + i * fsz;
   }
   // POCs run in batches: the fused path hands a batch of up to kBatchPocs POCs
   // (<= 32 (POC, refIdx) pairs) to one vame_affine_me_batch call, so they share
   // launches; --per-launch keeps the reference's one launch per (refIdx, PRED)
   const int B = J.per_launch ? 1 : kBatchPocs;
+  std::vector<std::vector<int>> batches;
+  for (size_t i = 0, pairs = 0; i < J.pocs.size(); i++) {
+    const int n = std::min(4, J.pocs[i]);
+    if (batches.empty() || (int)batches.back().size() == B || pairs + n > 32) {
+      batches.push_back({});
+      pairs = 0;
+    }
+    batches.back().push_back(J.pocs[i]);
+    pairs += n;
+  }
+  // Frames go up on their own stream from a thread of their own, batch by
+  // batch ahead of the kernels (copies from pageable host memory block the
+  // calling thread, so the launching thread never waits for them); batch b's
+  // kernels wait for upEv[b] on the device.
+  std::vector<hipEvent_t> upEv(batches.size());
+  for (auto& e : upEv) GPU_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  std::mutex upMu;
+  std::condition_variable upCv;
+  size_t upDone = 0;      // batches whose uploads are issued and whose event is recorded
+  bool upFailed = false;
+  struct Joiner {
+    std::thread t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } uploader;
+  uploader.t = std::thread([&] {
+    hipError_t e = hipSetDevice(J.device);
+    std::set<const uint16_t*> uploaded;
+    auto put = [&](uint16_t* dst, const uint16_t* src) {
+      if (e == hipSuccess && uploaded.insert(dst).second)
+        e = hipMemcpyAsync(dst, src, fsz * 2, hipMemcpyHostToDevice, up);
+    };
+    for (size_t b = 0; b < batches.size() && e == hipSuccess; b++) {
+      {
+        std::lock_guard<std::mutex> g(S->mu);
+        if (S->failed) break;
+      }
+      for (int p : batches[b]) {
+        put(dorig[p], J.orig + (size_t)(p - 1) * fsz);
+        int refs[4];
+        const int n = vame_ref_list(p, refs);
+        for (int r = 0; r < n; r++) put(drecon[refs[r]], J.recon + (size_t)refs[r] * fsz);
+      }
+      if (e == hipSuccess) e = hipEventRecord(upEv[b], up);
+      std::lock_guard<std::mutex> g(upMu);
+      if (e == hipSuccess) upDone = b + 1;
+      upCv.notify_all();
+    }
+    std::lock_guard<std::mutex> g(upMu);
+    upFailed = e != hipSuccess || upDone < batches.size();
+    upCv.notify_all();
+  });
   char* dres = nullptr;  // two batch slots of B POC layouts each
   GPU_CHECK(hipMalloc(&dres, 2 * (size_t)B * J.L->bytes), "hipMalloc results");
-  // two slots: batch k+1 is enqueued before the host waits for batch k's copies
-  hipEvent_t e0[2], e1[2], copied[2];
+  // two slots: batch k+1 is enqueued before the host waits for batch k's
+  // copies, which run on their own stream while batch k+1 computes (batch
+  // k+2 reuses the slot only after the host saw those copies complete)
+  hipEvent_t e0[2], e1[2], computed[2], copied[2];
   for (int i = 0; i < 2; i++) {
     GPU_CHECK(hipEventCreate(&e0[i]), "hipEventCreate");
     GPU_CHECK(hipEventCreate(&e1[i]), "hipEventCreate");
+    GPU_CHECK(hipEventCreateWithFlags(&computed[i], hipEventDisableTiming), "hipEventCreate");
     GPU_CHECK(hipEventCreateWithFlags(&copied[i], hipEventDisableTiming), "hipEventCreate");
   }
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evs[2];  // per-launch timing events
   std::vector<Slab*> pending;
   int pslot = 0;
+  hipEvent_t tStart, tFirst, tLast;  // trace: stream start, first and last kernel boundary
+  GPU_CHECK(hipEventCreate(&tStart), "hipEventCreate");
+  GPU_CHECK(hipEventCreate(&tFirst), "hipEventCreate");
+  GPU_CHECK(hipEventCreate(&tLast), "hipEventCreate");
+  GPU_CHECK(hipEventRecord(tStart, st), "hipEventRecord");
+  const double w2 = now_s();
+  double wFirst = 0, kernelSum = 0;
+  int late = 0;  // trace: batches issued after the previous one had finished on the GPU
+  std::vector<hipEvent_t> gs(batches.size()), ge(batches.size());  // trace: per-batch GPU boundaries
 
   // waits for a slot's copies, collects its kernel times, hands the slabs to the writer
   auto finish = [&](std::vector<Slab*>& batch, int slot) -> bool {
@@ -404,6 +477,7 @@ void gpu_worker(Job J) {
     } else {
       if (hipEventElapsedTime(&ms, e0[slot], e1[slot]) != hipSuccess) return false;
       batch[0]->fused_ns = ms * 1e6f;  // the batch's kernel time, reported once
+      kernelSum += ms;
     }
     std::lock_guard<std::mutex> g(S->mu);
     for (Slab* s : batch) S->done[s->poc] = s;
@@ -411,15 +485,11 @@ void gpu_worker(Job J) {
     return true;
   };
 
-  int k = 0;
-  for (size_t i0 = 0; i0 < J.pocs.size();) {
-    const int slot = k++ & 1;
+  for (size_t k = 0; k < batches.size(); k++) {
+    const int slot = (int)(k & 1);
     std::vector<Slab*> batch;
-    int pairs = 0;
-    while (i0 < J.pocs.size() && (int)batch.size() < B) {
-      const int p = J.pocs[i0];
+    for (int p : batches[k]) {
       const int n = std::min(4, p);
-      if (!batch.empty() && pairs + n > 32) break;
       Slab* slab = nullptr;
       {
         std::unique_lock<std::mutex> g(S->mu);
@@ -432,8 +502,25 @@ void gpu_worker(Job J) {
       slab->poc = p;
       slab->nrefs = n;
       batch.push_back(slab);
-      pairs += n;
-      i0++;
+    }
+    {  // this batch's frames: issued by the uploader, then waited for on the device
+      std::unique_lock<std::mutex> g(upMu);
+      upCv.wait(g, [&] { return upDone > k || upFailed; });
+      if (upDone <= k) {
+        fail(S, "upload frames failed");
+        return;
+      }
+    }
+    GPU_CHECK(hipStreamWaitEvent(st, upEv[k], 0), "hipStreamWaitEvent");
+    if (trace && k > 0 && hipEventQuery(computed[slot ^ 1]) == hipSuccess) late++;  // the GPU waited for this thread
+    if (trace) {
+      GPU_CHECK(hipEventCreate(&gs[k]), "hipEventCreate");
+      GPU_CHECK(hipEventCreate(&ge[k]), "hipEventCreate");
+      GPU_CHECK(hipEventRecord(gs[k], st), "hipEventRecord");
+    }
+    if (k == 0) {
+      GPU_CHECK(hipEventRecord(tFirst, st), "hipEventRecord");
+      wFirst = now_s();
     }
     auto base = [&](int j) { return dres + ((size_t)slot * B + j) * J.L->bytes; };
     if (J.per_launch) {
@@ -485,11 +572,14 @@ void gpu_worker(Job J) {
                  "vame_affine_me_batch");
       GPU_CHECK(hipEventRecord(e1[slot], st), "hipEventRecord");
     }
-    // stream order: this batch's kernels run after the previous batch's copies read its slot
+    if (trace) GPU_CHECK(hipEventRecord(ge[k], st), "hipEventRecord");
+    GPU_CHECK(hipEventRecord(computed[slot], st), "hipEventRecord");
+    if (k + 1 == batches.size()) GPU_CHECK(hipEventRecord(tLast, st), "hipEventRecord");
+    GPU_CHECK(hipStreamWaitEvent(dn, computed[slot], 0), "hipStreamWaitEvent");
     for (size_t j = 0; j < batch.size(); j++)
-      GPU_CHECK(hipMemcpyAsync(batch[j]->host, base((int)j), J.L->bytes, hipMemcpyDeviceToHost, st),
+      GPU_CHECK(hipMemcpyAsync(batch[j]->host, base((int)j), J.L->bytes, hipMemcpyDeviceToHost, dn),
                 "D2H");
-    GPU_CHECK(hipEventRecord(copied[slot], st), "hipEventRecord");
+    GPU_CHECK(hipEventRecord(copied[slot], dn), "hipEventRecord");
     if (!pending.empty() && !finish(pending, pslot)) {
       fail(S, "waiting for results failed");
       return;
@@ -501,6 +591,33 @@ void gpu_worker(Job J) {
     fail(S, "waiting for results failed");
     return;
   }
+  if (trace) {
+    float toFirst = 0, span = 0;
+    (void)hipEventElapsedTime(&toFirst, tStart, tFirst);
+    (void)hipEventElapsedTime(&span, tFirst, tLast);
+    fprintf(stderr,
+            "[trace] worker %d: host create %.1f ms, allocations %.1f ms, first launch issued at %.1f ms, "
+            "results in at %.1f ms; GPU: stream start -> first launch %.1f ms, first launch -> last "
+            "kernel %.1f ms, kernels %.1f ms (gaps %.1f ms)\n",
+            J.worker, (w1 - w0) * 1e3, (w2 - w1) * 1e3, (wFirst - w0) * 1e3, (now_s() - w0) * 1e3, toFirst,
+            span, kernelSum, span - kernelSum);
+    fprintf(stderr, "[trace] worker %d: %d of %zu batches issued after the previous one had finished; gaps (ms):",
+            J.worker, late, batches.size());
+    for (size_t b = 1; b < batches.size(); b++) {
+      float g = 0, len = 0;
+      (void)hipEventElapsedTime(&g, ge[b - 1], gs[b]);
+      (void)hipEventElapsedTime(&len, gs[b], ge[b]);
+      fprintf(stderr, " %.2f/%.1f", g, len);
+    }
+    fprintf(stderr, "\n");
+    for (size_t b = 0; b < batches.size(); b++) {
+      (void)hipEventDestroy(gs[b]);
+      (void)hipEventDestroy(ge[b]);
+    }
+  }
+  (void)hipEventDestroy(tStart);
+  (void)hipEventDestroy(tFirst);
+  (void)hipEventDestroy(tLast);
   for (int i = 0; i < 2; i++) {
     for (auto& e : evs[i]) {
       (void)hipEventDestroy(e.first);
@@ -508,11 +625,16 @@ void gpu_worker(Job J) {
     }
     (void)hipEventDestroy(e0[i]);
     (void)hipEventDestroy(e1[i]);
+    (void)hipEventDestroy(computed[i]);
     (void)hipEventDestroy(copied[i]);
   }
-  for (auto& kv : dorig) (void)hipFree(kv.second);
-  for (auto& kv : drecon) (void)hipFree(kv.second);
+  if (uploader.t.joinable()) uploader.t.join();
+  for (auto& e : upEv) (void)hipEventDestroy(e);
+  (void)hipFree(origBlk);
+  (void)hipFree(reconBlk);
   (void)hipFree(dres);
+  (void)hipStreamDestroy(up);
+  (void)hipStreamDestroy(dn);
   (void)hipStreamDestroy(st);
   vame_destroy(ctx);
 }
@@ -783,6 +905,9 @@ int main(int argc, char** argv) {
   }
   print_timestamp("FINISH GPU KERNEL");
   const double overall = now_s() - t0;
+  if (getenv("VAME_CLI_TRACE") && atoi(getenv("VAME_CLI_TRACE")) != 0)
+    fprintf(stderr, "[trace] workers started %.1f ms after reading; overall %.1f ms, log writing %.1f ms\n",
+            (t0 - t_read0 - read_s) * 1e3, overall * 1e3, log_s * 1e3);
 
   // main_aux_functions.h:1416-1446 reportTimingResults (ns; float like the reference)
   printf("=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=\n");

@@ -32,6 +32,7 @@ Without a launcher, `--gpus N` starts the N ranks itself (vame.launch).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import queue
@@ -156,11 +157,51 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
         orig = read(a.orig, pocs[0] - 1, pocs[-1] - pocs[0] + 1)
         recon = read(a.recon, need[0], need[-1] - need[0] + 1)
     T["read_csv_s"] = time.perf_counter() - t - T.get("index_others_s", 0.0)
-    if blocks:
-        up = lambda f: torch.from_numpy(np.ascontiguousarray(f).view(np.int16)).to(device)  # noqa: E731
-        d_orig = {p: up(orig[p - pocs[0]]) for p in pocs}
-        d_recon = {q: up(recon[q - need[0]]) for q in need}
-        del orig, recon
+
+    # frames go to the device launch by launch, ahead of the kernels, from a
+    # thread and on a stream of their own (copies from pageable memory block
+    # the calling thread, so the launching thread never waits for them); the
+    # compute stream waits for each launch's upload event.  Results come back
+    # on a third stream, overlapping the next launch.
+    batches = list(launch_batches(blocks))
+    compute = torch.cuda.current_stream(device) if cuda else None
+    upstream = torch.cuda.Stream(device) if cuda else None
+    dnstream = torch.cuda.Stream(device) if cuda else None
+    up_ready = [threading.Event() for _ in batches]
+    up_ev = [None] * len(batches)
+    up_err, up_stop = [], threading.Event()
+
+    def uploader():
+        def frame(store, key, host):
+            if key not in store:
+                t = torch.from_numpy(np.ascontiguousarray(host).view(np.int16))
+                if cuda:
+                    t = t.to(device, non_blocking=True)
+                    t.record_stream(compute)
+                store[key] = t
+        try:
+            with (torch.cuda.device(device) if cuda else contextlib.nullcontext()), \
+                    (torch.cuda.stream(upstream) if cuda else contextlib.nullcontext()):
+                for b, batch in enumerate(batches):
+                    if up_stop.is_set():
+                        break
+                    for poc, refs in batch:
+                        rl = ref_list(poc)
+                        frame(d_orig, poc, orig[poc - pocs[0]])
+                        for r in refs:
+                            frame(d_recon, rl[r], recon[rl[r] - need[0]])
+                    if cuda:
+                        up_ev[b] = torch.cuda.Event()
+                        up_ev[b].record(upstream)
+                    up_ready[b].set()
+        except Exception as e:  # surfaced by the launching thread
+            up_err.append(e)
+        finally:
+            for ev in up_ready:
+                ev.set()
+
+    up_th = threading.Thread(target=uploader, daemon=True)
+    up_th.start()
 
     # ---- who writes what: rank 0 appends to the final files as it goes; with
     # --shard-logs every other rank formats its block into host memory (a
@@ -203,13 +244,18 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
 
     # ---- the hot path: this block's launches
     spans = []
-    for batch in launch_batches(blocks):
+    for b, batch in enumerate(batches):
+        up_ready[b].wait()
+        if up_err:
+            up_stop.set()
+            raise up_err[0]
         jobs = []
         for poc, refs in batch:
             rl = ref_list(poc)
             jobs.append((d_orig[poc], [d_recon[rl[r]] for r in refs], lambda_for_poc(a.qp, poc),
                          engine.alloc_poc(len(refs), modes)))
         if cuda:
+            compute.wait_event(up_ev[b])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         engine.affine_me_batch(jobs, modes, a.extra)
@@ -221,24 +267,32 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
             if slot < 0:
                 break
             host = []
-            for i, job in enumerate(jobs):
-                h = {}
-                for key, (c, p) in job[3].items():
-                    hc = slots.host_like(slot, (i, key, 0), c)
-                    hp = slots.host_like(slot, (i, key, 1), p)
-                    hc.copy_(c, non_blocking=cuda)
-                    hp.copy_(p, non_blocking=cuda)
-                    h[key] = (hc, hp)
-                host.append(h)
-            ev = None
             if cuda:
-                ev = torch.cuda.Event()
-                ev.record()
+                dnstream.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(dnstream) if cuda else contextlib.nullcontext():
+                for i, job in enumerate(jobs):
+                    h = {}
+                    for key, (c, p) in job[3].items():
+                        hc = slots.host_like(slot, (i, key, 0), c)
+                        hp = slots.host_like(slot, (i, key, 1), p)
+                        hc.copy_(c, non_blocking=cuda)
+                        hp.copy_(p, non_blocking=cuda)
+                        if cuda:  # the launch's buffers stay allocated until the copy ran
+                            c.record_stream(dnstream)
+                            p.record_stream(dnstream)
+                        h[key] = (hc, hp)
+                    host.append(h)
+                ev = None
+                if cuda:
+                    ev = torch.cuda.Event()
+                    ev.record(dnstream)
             work.put((ev, slot, batch, host))
         elif a.log:  # gather path: compact records stay on this GPU until the gather
             slab_parts.append(shard.pack([j[3] for j in jobs], None, device, modes=modes))
     work.put(None)
     th.join()
+    up_stop.set()
+    up_th.join()
     if err:
         raise err[0]
     if cuda:
