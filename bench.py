@@ -16,12 +16,17 @@ itself (fresh child processes, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
 started before anything touches the GPU; backend nccl = RCCL over xGMI, or
 VAME_DIST_BACKEND=gloo to rehearse several ranks on one GPU); under a launcher
 (torchrun) that set WORLD_SIZE, WORLD_SIZE must equal --gpus.  Every rank codes the
-contiguous (POC, refIdx) pair block shard.pair_shard(n, world, rank) of ONE sequence (the same
-synthetic seed on every rank), with no collective on the data path.
-  c2 / c3 / c4 scale weakly: the first P x N (POC, refIdx) pairs of the
-               sequence, P = the pairs of `frames` POCs, so every rank codes
-               exactly P pairs (c2: 3, c3 / c4: 114; at N = 1 exactly the config);
-  c5           scales strongly: 240 POCs of 3840x2160 in all (configs[4]).
+frames of its own share, with no collective on the data path.
+  c2 / c3 / c4 scale weakly: every rank codes exactly the config's (POC,
+               refIdx) pairs (c2: 3, c3 / c4: 114; at N = 1 exactly the config):
+               --weak streams (default): N independent sequences, one per
+               rank (own synthetic texture, the same camera motion);
+               --weak sequence: the first P x N pairs of ONE sequence cut into
+               contiguous pair blocks shard.pair_shard(n, world, rank) (rank k
+               then codes POCs up to ~3k deep, whose long-term references
+               converge more slowly: a content effect, not a scaling one);
+  c5           scales strongly: 240 POCs of 3840x2160 in all (configs[4]),
+               contiguous pair blocks of one sequence.
 After the timed steps the decision records go to rank 0 in one RCCL gather
 (timed and reported separately as `gather`), and rank 0 recomputes the first
 and last POC of every rank's block and checks the gathered records byte for
@@ -72,6 +77,8 @@ def main():
     ap.add_argument("--qp", type=int, default=None)
     ap.add_argument("--frames", type=int, default=None,
                     help="sequence length (c5: total POCs; c2-c4: POCs per GPU)")
+    ap.add_argument("--weak", default="streams", choices=("streams", "sequence"),
+                    help="weak-scaling data (c2-c4): a sequence per rank, or pair blocks of one sequence")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rank-only", type=int, default=None, metavar="K",
                     help="diagnostic: run only rank K's block of a --gpus N job, alone on GPU 0 "
@@ -114,11 +121,13 @@ def main():
     # first frames_pairs x N pairs of one sequence, cut at pair granularity);
     # strong scaling: the config's whole sequence over the N ranks
     from vame.shard import frames_for_pairs, sequence_pairs
-    n_pairs = sequence_pairs(cfg["frames"]) * world if cfg["scaling"] == "weak" else None
+    weak = cfg["scaling"] == "weak"
+    streams = weak and args.weak == "streams"
+    n_pairs = sequence_pairs(cfg["frames"]) * (1 if streams else world) if weak else None
     n_frames = frames_for_pairs(n_pairs) if n_pairs is not None else cfg["frames"]
     ncps = (2, 3) if modes & 2 else (2,)
     eng = Engine(W, H, dev.index)
-    run = ShardRun(eng, W, H, qp, n_frames, modes, world, rank, dev, n_pairs=n_pairs)
+    run = ShardRun(eng, W, H, qp, n_frames, modes, world, rank, dev, n_pairs=n_pairs, streams=streams)
     log(f"[rank {rank}] POCs {run.pocs[:1]}..{run.pocs[-1:]} ({run.pairs} pairs) of {n_frames}, "
         f"frames synthesized in {run.synth_s:.1f}s")
     acc = pair_accounting(W, H, ncps)
@@ -235,7 +244,8 @@ def main():
                    "pairs_per_step_rank0": run.pairs, "rows_per_step_rank0": rows_per_step,
                    "rows_per_step_all": rows_total / args.steps,
                    "modes": "2cp+3cp" if modes & 2 else "2cp",
-                   "parallelism": f"frame-shard x{world} (pair_shard of one sequence)",
+                   "parallelism": (f"frame-shard x{world} (a sequence of its own per rank)" if streams else
+                                   f"frame-shard x{world} (pair_shard of one sequence)"),
                    **({"rank_only": {"rank": rank, "of": world}} if args.rank_only is not None else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": prof.get("traffic"),

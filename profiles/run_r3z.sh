@@ -1,0 +1,24 @@
+# Weak-scaling forecast for the driver's SCALE run (c2, bench.py --gpus N):
+# every rank's block of an N-rank job alone on this one GPU (--rank-only K),
+# N = 2, 4, 8.  The job's time is the slowest rank's.
+set -o pipefail
+O=gpurun_out/r3z; mkdir -p $O
+timeout -k 10 120 python bench.py --no-cpu-baseline --no-spans > $O/n1.json 2> $O/n1.err || exit 1
+for N in 2 4 8; do
+  for K in $(seq 0 $((N - 1))); do
+    timeout -k 10 120 python bench.py --no-cpu-baseline --no-spans --gpus $N --rank-only $K > $O/n${N}_r$K.json 2> $O/n${N}_r$K.err || { tail -5 $O/n${N}_r$K.err; exit 1; }
+  done
+done
+python3 - <<'PY'
+import json, glob
+O = "gpurun_out/r3z"
+n1 = json.load(open(f"{O}/n1.json"))
+print("N=1", round(n1["ms_per_step"], 4), "ms/step", n1["config"]["pairs_per_step_rank0"], "pairs")
+for N in (2, 4, 8):
+    rs = [json.load(open(f"{O}/n{N}_r{k}.json")) for k in range(N)]
+    ms = [r["ms_per_step"] for r in rs]
+    rows = sum(r["config"]["rows_per_step_rank0"] for r in rs)
+    print(f"N={N}", [round(m, 4) for m in ms], "max", round(max(ms), 4),
+          "forecast efficiency", round(rows / max(ms) / (N * n1["value"] / 1e3), 4),
+          "checks", all(r["gather"]["check"]["byte_identical"] for r in rs))
+PY

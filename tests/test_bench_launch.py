@@ -34,12 +34,14 @@ def test_gpus_must_be_positive():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-def test_bench_gpus2_launches_two_ranks():
+@pytest.mark.parametrize("weak", ["streams", "sequence"])
+def test_bench_gpus2_launches_two_ranks(weak):
     """`python bench.py --gpus 2 --config c2 --steps 3` with no launcher: two
     ranks (gloo, one GPU), one JSON line from rank 0 with n_gpus 2, the world
-    it ran in, and the gathered records byte-identical to rank 0's recompute."""
+    it ran in, and the gathered records byte-identical to rank 0's recompute
+    (both weak-scaling forms: a sequence per rank, pair blocks of one)."""
     r = run_bench(["--gpus", "2", "--config", "c2", "--steps", "3", "--warmup", "1",
-                   "--no-cpu-baseline"], {"VAME_DIST_BACKEND": "gloo"}, timeout=280)
+                   "--no-cpu-baseline", "--weak", weak], {"VAME_DIST_BACKEND": "gloo"}, timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -48,3 +50,7 @@ def test_bench_gpus2_launches_two_ranks():
     assert d["config"]["rows_per_step_all"] == 2 * d["config"]["rows_per_step_rank0"]
     assert d["gather"]["check"]["byte_identical"] is True
     assert d["step_ms"]["min"] <= d["step_ms"]["median"] <= d["step_ms"]["max"]
+    assert d["config"]["pairs_per_step_rank0"] == 3
+    assert d["gather"]["check"]["cut_pocs"] == []  # sequence: POC 1-2 | POC 3, no cut
+    assert d["config"]["parallelism"].endswith("(a sequence of its own per rank)" if weak == "streams"
+                                               else "(pair_shard of one sequence)")

@@ -330,6 +330,46 @@ def test_bench_shard_path_two_ranks_equals_single_process(tmp_path):
     assert got["bytes"] == 4 * got["slabs"][0].numel()
 
 
+def streams_worker(rank, world, port, outdir):
+    """bench.py's default weak scaling (--weak streams): every rank codes the
+    same pairs of a sequence of its own; gather into rank 0 and its check."""
+    from vame.seqrun import ShardRun
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    run = ShardRun(OracleEngine(SEQ_W, SEQ_H), SEQ_W, SEQ_H, 27, 2, 1, world, rank,
+                   torch.device("cpu"), seed=11, n_pairs=3, streams=True)
+    run.step()
+    slabs, nbytes = run.gather()
+    if rank == 0:
+        torch.save({"slabs": slabs, "check": run.verify(slabs, full=True), "blocks": run.blocks},
+                   os.path.join(outdir, "streams.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_weak_streams_two_ranks(tmp_path):
+    """--weak streams on 2 gloo ranks: both ranks code POC 1-2 (3 pairs, the
+    c2 shape) of their own sequence (seed_of(rank)); each gathered slab equals
+    a 1-rank run with that seed, the two differ, nothing is cut, and rank 0's
+    full recompute check passes."""
+    from vame.seqrun import ShardRun
+    port = free_port()
+    mp.spawn(streams_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    got = torch.load(os.path.join(tmp_path, "streams.pt"), weights_only=True)
+    assert got["blocks"] == [(1, [0]), (2, [0, 1])]
+    assert got["check"]["byte_identical"] and got["check"]["cut_pocs"] == []
+    assert [r for _, _, r in got["check"]["pocs"]] == [0, 0, 1, 1]
+    for r in range(2):
+        one = ShardRun(OracleEngine(SEQ_W, SEQ_H), SEQ_W, SEQ_H, 27, 2, 1, 2, r,
+                       torch.device("cpu"), seed=11, n_pairs=3, streams=True)
+        assert one.seed_of(r) == 11 + 7919 * r
+        one.step()
+        assert torch.equal(got["slabs"][r], one.slab()), r
+    assert not torch.equal(got["slabs"][0], got["slabs"][1])
+
+
 @pytest.mark.timeout(300)
 def test_rank_only_block_and_verify_own():
     """A --rank-only diagnostic (bench.py / vame.distrun): rank 1's block of a

@@ -359,8 +359,23 @@ void gpu_worker(Job J) {
   VAME_CHECK(vame_set_prof(ctx, J.prof ? 1 : 0), "vame_set_prof");
   hipStream_t st, up, dn;  // compute; frame uploads; result downloads
   GPU_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
-  GPU_CHECK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking), "hipStreamCreate");
-  GPU_CHECK(hipStreamCreateWithFlags(&dn, hipStreamNonBlocking), "hipStreamCreate");
+  // The copy streams are created with an explicit priority: created like the
+  // compute stream, one of them shared its hardware queue with it (HIP maps
+  // streams onto GPU_MAX_HW_QUEUES = 4 queues, and this process has five
+  // streams), so each batch's 285 MB result download at C5 (5.1 ms at PCIe
+  // rate) sat in front of the next batch's kernels: 0.30 s of idle GPU per
+  // 240 4K frames (VAME_CLI_TRACE).  VAME_CLI_COPY_PRIO=0 restores that.
+  const int copyPrio = getenv("VAME_CLI_COPY_PRIO") ? atoi(getenv("VAME_CLI_COPY_PRIO")) : 1;
+  if (copyPrio) {
+    int lo = 0, hi = 0;
+    GPU_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+    const int pr = copyPrio > 0 ? lo : hi;
+    GPU_CHECK(hipStreamCreateWithPriority(&up, hipStreamNonBlocking, pr), "hipStreamCreate");
+    GPU_CHECK(hipStreamCreateWithPriority(&dn, hipStreamNonBlocking, pr), "hipStreamCreate");
+  } else {
+    GPU_CHECK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking), "hipStreamCreate");
+    GPU_CHECK(hipStreamCreateWithFlags(&dn, hipStreamNonBlocking), "hipStreamCreate");
+  }
   const size_t fsz = (size_t)J.W * J.H;
   // frames: orig of each POC, recon of every label its ring holds -- allocated
   // here in two blocks, uploaded per batch (upload_frames below)

@@ -10,6 +10,13 @@ path.  The one exchange is the decision-record gather into rank 0
 (`shard.gather_to_root`, RCCL over xGMI), after which rank 0 can recompute a
 sample of every other rank's POCs and check the gathered records byte for byte.
 
+With `streams` every rank instead codes the same (POC, refIdx) pairs of a
+sequence of its own (seed_of(rank): the same camera motion over its own
+texture): N independent streams on N GPUs, the weak-scaling form in which each
+GPU's work is the 1-GPU configuration itself rather than a deeper cut of one
+sequence (whose later POCs reference frames up to 23 back and converge more
+slowly).
+
 The compute engine is injected (`engine` needs `alloc_poc`, `affine_me_batch`
 and `n_cus`): bench.py passes the HIP engine (vame.engine.Engine);
 tests/test_shard.py passes an oracle-backed stand-in to run this exact path
@@ -28,15 +35,18 @@ from .hostlogic import lambda_for_poc, ref_list
 
 class ShardRun:
     """Pair block `pair_shard(n_frames, world, rank, n_pairs)` of the sequence
-    (W, H, qp, n_frames, seed), coded with `engine` on `device`."""
+    (W, H, qp, n_frames, seed) -- or with `streams` all `n_pairs` of this
+    rank's own sequence -- coded with `engine` on `device`."""
 
     def __init__(self, engine, W: int, H: int, qp: int, n_frames: int, modes: int, world: int,
-                 rank: int, device, seed: int = 0x5EED, n_pairs: int | None = None):
+                 rank: int, device, seed: int = 0x5EED, n_pairs: int | None = None,
+                 streams: bool = False):
         self.eng, self.W, self.H, self.qp, self.n = engine, W, H, qp, n_frames
         self.n_pairs = n_pairs
         self.modes, self.world, self.rank, self.device, self.seed = modes, world, rank, device, seed
+        self.streams = streams
         self.n_cus = (engine.n_cus(0), engine.n_cus(1))
-        self.blocks = shard.pair_shard(n_frames, world, rank, n_pairs)
+        self.blocks = self.blocks_of(rank)
         self.pocs = [p for p, _ in self.blocks]
         t0 = time.perf_counter()
         self.jobs = self._jobs(self.blocks)
@@ -45,18 +55,29 @@ class ShardRun:
         # every rank's slab is padded to the largest shard's words (equal-size gather)
         self.words = max(shard.slab_words(self.layout(r)) for r in range(world))
 
+    def blocks_of(self, rank: int):
+        """`rank`'s (POC, [refIdx...]) block: its pair block of the one
+        sequence, or with `streams` the whole `n_pairs` of its own sequence."""
+        if self.streams:
+            return shard.pair_shard(self.n, 1, 0, self.n_pairs)
+        return shard.pair_shard(self.n, self.world, rank, self.n_pairs)
+
+    def seed_of(self, rank: int) -> int:
+        """The synthetic seed of `rank`'s frames: one sequence for all ranks,
+        or with `streams` a sequence per rank (same camera motion, own texture)."""
+        return self.seed + 7919 * rank if self.streams else self.seed
+
     def layout(self, rank: int):
         """`shard.unpack` layout of `rank`'s slab."""
-        return shard.block_layout(shard.pair_shard(self.n, self.world, rank, self.n_pairs), self.modes,
-                                  self.n_cus)
+        return shard.block_layout(self.blocks_of(rank), self.modes, self.n_cus)
 
-    def _jobs(self, blocks):
+    def _jobs(self, blocks, seed: int | None = None):
         """One engine job per (POC, [refIdx...]) entry; the job's results are
         keyed by the position in that refIdx list."""
         rps = {poc: [ref_list(poc)[i] for i in refs] for poc, refs in blocks}
         pocs = [p for p, _ in blocks]
         orig, recon = synth.synth_pocs(self.W, self.H, pocs, sorted({r for v in rps.values() for r in v}),
-                                       self.qp, self.seed)
+                                       self.qp, self.seed_of(self.rank) if seed is None else seed)
         up = lambda f: torch.from_numpy(f.view(np.int16)).to(self.device)  # noqa: E731
         d_recon = {p: up(f) for p, f in recon.items()}
         jobs = []
@@ -99,6 +120,8 @@ class ShardRun:
 
     def cut_pocs(self) -> list[int]:
         """POCs whose refIdx range is split between two ranks' pair blocks."""
+        if self.streams:  # every rank codes a sequence of its own
+            return []
         owners: dict[int, set] = {}
         for r in range(self.world):
             for poc, _ in shard.pair_shard(self.n, self.world, r, self.n_pairs):
@@ -113,7 +136,7 @@ class ShardRun:
         checked, ok = [], True
         cuts = set(self.cut_pocs())
         for r in range(self.world):
-            blocks = shard.pair_shard(self.n, self.world, r, self.n_pairs)
+            blocks = self.blocks_of(r)
             if not blocks:
                 continue
             idx = sorted(set(range(len(blocks))) if full else
@@ -125,7 +148,7 @@ class ShardRun:
             for k in range(0, len(idx), 8):  # recompute in batches of 8 block entries
                 part = idx[k:k + 8]
                 sample = [blocks[i] for i in part]
-                jobs = self._jobs(sample)
+                jobs = self._jobs(sample, self.seed_of(r))
                 self.eng.affine_me_batch(jobs, self.modes, 0)
                 for i, (poc, refs), job in zip(part, sample, jobs):
                     want = shard.pack([job[3]], None, self.device, modes=self.modes)
