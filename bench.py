@@ -280,6 +280,7 @@ def main():
                    "check": check},
     }
 
+    result["native"] = native_record()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"], result["parity_sample"] = cpu_baseline(run, acc, ncps, W, H, modes)
     if dist is not None:
@@ -289,6 +290,22 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def native_record() -> dict:
+    """The HIP library this run loaded, tied to the build that made it
+    (__graft_entry__.build() writes lib/build_record.json)."""
+    import hashlib
+    from vame import _lib
+    rec = {"lib": os.path.relpath(_lib.LIB_PATH, REPO),
+           "sha256": hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()}
+    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "build_record.json")
+    if os.path.exists(path):
+        b = json.load(open(path))
+        built = b.get("artefacts", {}).get("vvc-affine-gpu_amd/lib/libvame.so", {})
+        rec["build"] = {"git_head": b.get("git_head"), "mode": b.get("mode"),
+                        "matches_loaded_lib": built.get("sha256") == rec["sha256"]}
+    return rec
 
 
 def load_profile(config: str, avg_launch_ms: float) -> dict:
