@@ -54,3 +54,32 @@ def test_bench_gpus2_launches_two_ranks(weak):
     assert d["gather"]["check"]["cut_pocs"] == []  # sequence: POC 1-2 | POC 3, no cut
     assert d["config"]["parallelism"].endswith("(a sequence of its own per rank)" if weak == "streams"
                                                else "(pair_shard of one sequence)")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_under_torchrun():
+    """The driver's multi-GPU command form: `python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P
+    bench.py --gpus 2 ...` (gloo here: both ranks share the test box's GPU).
+    The launcher set WORLD_SIZE, so bench.py starts no ranks of its own."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    e = dict(os.environ, VAME_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "VAME_LAUNCHER"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(REPO, "bench.py"), "--gpus", "2", "--config", "c2", "--steps", "3",
+                        "--warmup", "1", "--no-cpu-baseline"], env=e, capture_output=True, text=True,
+                       timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world"] == {"size": 2, "backend": "gloo", "launcher": "external"}
+    assert d["gather"]["check"]["byte_identical"] is True
+    assert d["native"]["lib"].endswith("libvame.so")
