@@ -162,7 +162,8 @@ def main():
     for _ in range(args.warmup):
         run.step()
     barrier()
-    eng.set_timing(True)
+    ktiming = os.environ.get("VAME_BENCH_KTIMING", "1") != "0"  # diagnostic: 0 = no kernel events in the timed steps
+    eng.set_timing(ktiming)
     # one event per step boundary on the issuing stream: the per-step spread
     step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t_start = time.perf_counter()

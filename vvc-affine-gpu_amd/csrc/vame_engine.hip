@@ -4,6 +4,7 @@
 // management, :754-966 clSetKernelArg/clEnqueueNDRangeKernel for the four
 // kernel objects).  The host side here only builds the work-item templates,
 // packs one kernel-argument struct and enqueues on the caller's stream.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -208,24 +209,25 @@ void fill_common(KParams& kp, const vame_ctx* c, int extra) {
   kp.extra = extra;
 }
 
-// timing hooks (no-ops unless vame_set_timing(ctx, 1))
-int time_begin(vame_ctx* c, int cls, hipStream_t s) {
+// Per-kernel timing (vame_set_timing(ctx, 1)): the kernel's own dispatch
+// packet carries the start / stop events (hipExtLaunchKernel), so timing adds
+// no marker packets to the streams and the interval is the dispatch's own
+// execution, as rocprofv3 reports it (timed dispatches still cost ~0.8 % of a
+// c2 step, with or without the events' system-scope fence, as did the event
+// records around each launch used before).  Returns the (start, stop) pair for the
+// next launch of kernel class `cls`, or nulls with timing off.
+int time_events(vame_ctx* c, int cls, hipEvent_t& start, hipEvent_t& stop) {
+  start = stop = nullptr;
   if (!c->timing) return VAME_OK;
   auto& v = c->ev[cls];
   if (c->evUsed[cls] == v.size()) {
     std::pair<hipEvent_t, hipEvent_t> e;
-    // timing-only events: no system-scope fence (no cache writeback /
-    // invalidation between the kernels they bracket)
-    VAME_HIP(hipEventCreateWithFlags(&e.first, hipEventDisableSystemFence));
-    VAME_HIP(hipEventCreateWithFlags(&e.second, hipEventDisableSystemFence));
+    VAME_HIP(hipEventCreate(&e.first));
+    VAME_HIP(hipEventCreate(&e.second));
     v.push_back(e);
   }
-  VAME_HIP(hipEventRecord(v[c->evUsed[cls]].first, s));
-  return VAME_OK;
-}
-int time_end(vame_ctx* c, int cls, hipStream_t s) {
-  if (!c->timing) return VAME_OK;
-  VAME_HIP(hipEventRecord(c->ev[cls][c->evUsed[cls]].second, s));
+  start = v[c->evUsed[cls]].first;
+  stop = v[c->evUsed[cls]].second;
   c->evUsed[cls]++;
   return VAME_OK;
 }
@@ -365,11 +367,11 @@ int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool qua
     kb.items = c->dBig;
     kb.nItems = c->nBig;
     const unsigned grid = block_grid(c, 1, kb);
-    VAME_TRY(time_begin(c, 1, sBig));
-    hipLaunchKernelGGL(kernel_for<true>(c->prof, mode), dim3(grid),
-                       dim3(Cfg<128>::THREADS), 0, sBig, kb);
+    hipEvent_t t0, t1;
+    VAME_TRY(time_events(c, 1, t0, t1));
+    hipExtLaunchKernelGGL(kernel_for<true>(c->prof, mode), dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig,
+                          t0, t1, 0, kb);
     VAME_HIP(hipGetLastError());
-    VAME_TRY(time_end(c, 1, sBig));
     return VAME_OK;
   };
   auto quad = [&](const KParams& kp) -> int {
@@ -377,11 +379,11 @@ int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool qua
     kq.items = quadFull ? c->dQuad : c->dQuad + c->nQuadFull;
     kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
     const unsigned grid = block_grid(c, 0, kq);
-    VAME_TRY(time_begin(c, 0, sQuad));
-    hipLaunchKernelGGL(kernel_for<false>(c->prof, mode), dim3(grid),
-                       dim3(Cfg<64>::THREADS), 0, sQuad, kq);
+    hipEvent_t t0, t1;
+    VAME_TRY(time_events(c, 0, t0, t1));
+    hipExtLaunchKernelGGL(kernel_for<false>(c->prof, mode), dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad,
+                          t0, t1, 0, kq);
     VAME_HIP(hipGetLastError());
-    VAME_TRY(time_end(c, 0, sQuad));
     return VAME_OK;
   };
   for (size_t k = 0; k < kps.size(); k++) {
