@@ -98,3 +98,18 @@ def test_instrumentation_builds_compile(tmp_path, defs):
                         "-ffp-contract=off", "--cuda-device-only", "-c", *defs, "-o",
                         str(tmp_path / "ab.o"), src], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_build_record_matches_the_library():
+    """__graft_entry__.build() recompiles libvame.so and records its sha256 in
+    lib/build_record.json; bench.py reports whether the library it loaded is
+    that build's.  A record that no longer matches the library on disk means a
+    later build bypassed build() (skipped when no record was written)."""
+    import hashlib
+    rec_path = os.path.join(os.path.dirname(_lib.LIB_PATH), "build_record.json")
+    if not os.path.exists(rec_path) or os.environ.get("VAME_LIB"):
+        pytest.skip("no build record (library not built by __graft_entry__.build())")
+    rec = json.load(open(rec_path))
+    want = rec["artefacts"]["vvc-affine-gpu_amd/lib/libvame.so"]["sha256"]
+    assert hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest() == want
+    assert rec["mode"].startswith("rebuilt")
