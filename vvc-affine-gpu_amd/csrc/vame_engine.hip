@@ -47,7 +47,7 @@ struct vame_ctx {
   hipStream_t side = nullptr;   // second stream: 128-class items run beside the quadrant items
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   // optional per-kernel timing: (start, end) event pairs per kernel class
-  bool timing = false;
+  int timing = 0;
   // PROF on (vame_set_prof): the *_prof kernels
   bool prof = false;
   // VAME_JOIN_EACH=1: join the two streams after every launch of a batch
@@ -218,7 +218,7 @@ void fill_common(KParams& kp, const vame_ctx* c, int extra) {
 // next launch of kernel class `cls`, or nulls with timing off.
 int time_events(vame_ctx* c, int cls, hipEvent_t& start, hipEvent_t& stop) {
   start = stop = nullptr;
-  if (!c->timing) return VAME_OK;
+  if (!((c->timing >> cls) & 1)) return VAME_OK;
   auto& v = c->ev[cls];
   if (c->evUsed[cls] == v.size()) {
     std::pair<hipEvent_t, hipEvent_t> e;
@@ -604,7 +604,7 @@ int vame_set_prof(vame_ctx* c, int enable) {
 
 int vame_set_timing(vame_ctx* c, int enable) {
   if (!c) return VAME_E_INVALID;
-  c->timing = enable != 0;
+  c->timing = enable == 2 ? 1 : enable != 0 ? 3 : 0;  // kernel classes timed (bit 0 quadrant, bit 1 128-class)
   c->evUsed[0] = c->evUsed[1] = 0;
   return VAME_OK;
 }

@@ -65,7 +65,8 @@ class Engine:
         affine.cl:168); vame_set_prof."""
         check(lib().vame_set_prof(self._h, int(enable)))
 
-    def set_timing(self, enable: bool) -> None:
+    def set_timing(self, enable) -> None:
+        """True / 1: time every kernel class; 2: the quadrant kernel only; 0: off."""
         check(lib().vame_set_timing(self._h, int(enable)))
 
     def get_timing(self, kernel_class: int, reset: bool = True):
