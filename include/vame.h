@@ -106,11 +106,12 @@ int vame_affine_me_batch(vame_ctx* ctx, const vame_poc_job* jobs, int njobs, int
 int vame_set_prof(vame_ctx* ctx, int enable);
 
 /* Device-side kernel timing (the reference's per-PRED kernelExecutionTime,
- * main.cpp:856-866): when enabled, every kernel launch is bracketed by hipEvents
- * on the stream it runs on.  kernel_class 0 = quadrant work items
+ * main.cpp:856-866): when enabled, every kernel launch carries hipEvents in its
+ * own dispatch on the stream it runs on.  kernel_class 0 = quadrant work items
  * (affine_me_quad), 1 = 128-class work items (affine_me_ctu).
- * vame_get_timing waits for the recorded launches and returns their summed
- * duration and count since the last reset. */
+ * enable = 2 times the quadrant kernel only (its dispatches carry the events;
+ * the 128-class launches run untimed).  vame_get_timing waits for the recorded
+ * launches and returns their summed duration and count since the last reset. */
 int vame_set_timing(vame_ctx* ctx, int enable);
 int vame_get_timing(vame_ctx* ctx, int kernel_class, double* total_ms, int* launches, int reset);
 
