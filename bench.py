@@ -246,9 +246,17 @@ def main():
         # rank 0's per-step GPU times (HIP events at the step boundaries)
         "step_ms": {"median": step_ms[len(step_ms) // 2], "min": step_ms[0], "max": step_ms[-1]},
         "world": {"size": world, "backend": "none" if dist is None else dist.get_backend(),
-                  "launcher": os.environ.get("VAME_LAUNCHER", "external" if world > 1 else "none")},
+                  "launcher": os.environ.get("VAME_LAUNCHER", "external" if world > 1 else "none"),
+                  # VAME_FORCE_PG=1: a one-rank process group, so the N-GPU
+                  # collectives (init, all_reduce, gather) run on one GPU
+                  "forced_pg": args.rank_only is None and world == 1 and dist is not None},
         "higher_is_better": True,
         "scaling": cfg["scaling"],
+        # which multi-GPU form this line measures: weak scaling over
+        # independent sequences ("streams", the default) or over pair blocks
+        # of one sequence ("sequence"); c5 is the north star's frame shard of
+        # one 240-frame sequence (strong scaling)
+        "scaling_form": ("streams" if streams else "sequence") if weak else "frame-shard",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
@@ -260,6 +268,13 @@ def main():
                    "modes": "2cp+3cp" if modes & 2 else "2cp",
                    "parallelism": (f"frame-shard x{world} (a sequence of its own per rank)" if streams else
                                    f"frame-shard x{world} (pair_shard of one sequence)"),
+                   "scaling_form_note": ("N independent sequences (each rank codes the 1-GPU config "
+                                         "on its own synthetic sequence); the frame shard of one "
+                                         "sequence is --config c5" if streams else
+                                         "the first P x N pairs of one sequence in contiguous pair "
+                                         "blocks (deeper POCs on higher ranks)" if weak else
+                                         "240 POCs of one sequence in contiguous pair blocks over "
+                                         "the ranks"),
                    **({"rank_only": {"rank": rank, "of": world}} if args.rank_only is not None else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": prof.get("traffic"),

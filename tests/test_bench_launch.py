@@ -32,6 +32,90 @@ def test_gpus_must_be_positive():
     assert r.returncode != 0 and "--gpus" in r.stderr
 
 
+POISON = """
+import sys, torch
+def boom(*a, **k):
+    raise RuntimeError("torch.cuda touched in the launcher parent")
+for name in ("device_count", "is_available", "init", "set_device", "current_device", "_lazy_init",
+             "synchronize", "get_device_properties"):
+    setattr(torch.cuda, name, boom)
+sys.path.insert(0, {pkg!r})
+from vame.launch import launch_ranks
+rc = launch_ranks(2, ["-c", "import os, sys; sys.exit(0 if os.environ['WORLD_SIZE'] == '2' and "
+                            "os.environ['LOCAL_RANK'] in ('0', '1') else 3)"], "nccl", "poison-test")
+sys.exit(rc)
+"""
+
+
+def fake_topology(root, gpus, cpus=1):
+    """A KFD topology tree: CPU nodes (gpu_id 0) then GPU nodes."""
+    for k in range(cpus + gpus):
+        d = root / str(k)
+        d.mkdir()
+        (d / "gpu_id").write_text("0\n" if k < cpus else f"{1000 + k}\n")
+    return str(root)
+
+
+def test_launcher_never_touches_torch_cuda(tmp_path):
+    """the nccl branch of launch_ranks must not initialise
+    the GPU runtime in the parent that spawns the ranks.  Every torch.cuda
+    entry point raises in this parent; the 2 ranks start and exit 0 (with a
+    fake 2-GPU topology, and with none at all)."""
+    pkg = os.path.join(REPO, "vvc-affine-gpu_amd")
+    code = POISON.format(pkg=pkg)
+    for env in ({"VAME_KFD_TOPOLOGY": fake_topology(tmp_path, 2)},
+                {"VAME_KFD_TOPOLOGY": str(tmp_path / "absent")}):
+        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env),
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert "touched" not in r.stderr
+
+
+def test_launcher_refuses_more_ranks_than_gpus(tmp_path):
+    pkg = os.path.join(REPO, "vvc-affine-gpu_amd")
+    code = POISON.format(pkg=pkg)
+    r = subprocess.run([sys.executable, "-c", code],
+                       env=dict(os.environ, VAME_KFD_TOPOLOGY=fake_topology(tmp_path, 1)),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "2 ranks but 1 GPUs visible" in r.stderr
+
+
+def test_visible_gpu_count(tmp_path, monkeypatch):
+    from vame.launch import visible_gpu_count
+    topo = fake_topology(tmp_path, 8, cpus=2)
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert visible_gpu_count(topo) == 8
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "3,5")
+    assert visible_gpu_count(topo) == 2
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "1")
+    assert visible_gpu_count(topo) == 1
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")  # empty: no restriction
+    assert visible_gpu_count(topo) == 8
+    assert visible_gpu_count(str(tmp_path / "none")) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_forced_rccl_group():
+    """the RCCL branch on one MI355X.  VAME_FORCE_PG=1 forms
+    a real one-rank nccl process group, so init_process_group("nccl",
+    device_id=...), the device-tensor all_reduce of the timing and the
+    dist.gather of the decision records into rank 0 all run through RCCL;
+    rank 0 then recomputes its block and checks the gathered records."""
+    r = run_bench(["--config", "c2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"],
+                  {"VAME_FORCE_PG": "1"}, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["world"]["backend"] == "nccl" and d["world"]["forced_pg"] is True and d["world"]["size"] == 1
+    assert d["gather"]["backend"] == "nccl"
+    assert d["gather"]["check"]["byte_identical"] is True and len(d["gather"]["check"]["pocs"]) >= 1
+    assert d["n_gpus"] == 1 and d["scaling_form"] == "streams"
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("weak", ["streams", "sequence"])

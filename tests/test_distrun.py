@@ -173,6 +173,69 @@ def test_gathered_logs_byte_identical(seq, world):
     assert len(compare_dirs(run_ranks(seq, world, f"gather{world}"), seq / "expected")) == 40
 
 
+def self_gather_worker(rank, world, port, argv, table_path):
+    rank_worker(rank, world, port, argv, table_path)
+
+
+@pytest.mark.timeout(600)
+def test_one_rank_group_gathers_its_own_records(seq):
+    """A one-rank process group (what VAME_FORCE_PG=1 forms): rank 0's records
+    take the gather path -- packed per launch with the deferred device-side
+    check, gathered through the collective, unpacked and written from the
+    slab -- and the 40 files equal the reference writer's."""
+    out = seq / "selfgather"
+    out.mkdir()
+    argv = ["-f", str(SEQ["n"]), "-s", f"{SEQ['W']}x{SEQ['H']}", "-q", str(SEQ["qp"]),
+            "-o", str(seq / "orig.csv"), "-r", str(seq / "recon.csv"), "-l", str(out / "log")]
+    from vame.launch import free_port
+    mp.spawn(self_gather_worker, args=(1, free_port(), argv, str(seq / "table.pt")), nprocs=1, join=True)
+    assert len(compare_dirs(out, seq / "expected")) == 40
+
+
+def test_pack_deferred_check():
+    """shard.pack with a device flag collects the compact-form check without a
+    host read; check_flag raises once a record does not fit."""
+    n = 5
+    good = {(0, "FULL_2CP"): (torch.arange(n, dtype=torch.int64), torch.zeros((n, 7), dtype=torch.int32))}
+    flag = torch.zeros((), dtype=torch.bool)
+    shard.pack([good], validate=flag, modes=None)
+    shard.check_flag(flag)
+    bad_cost = {(0, "FULL_2CP"): (torch.full((n,), 2**31, dtype=torch.int64), torch.zeros((n, 7), dtype=torch.int32))}
+    cp = torch.zeros((n, 7), dtype=torch.int32)
+    cp[2, 6] = 4  # a 2-CP record with LB != 0
+    bad_lb = {(0, "HALF_2CP"): (torch.zeros(n, dtype=torch.int64), cp)}
+    for bad in (bad_cost, bad_lb):
+        f = torch.zeros((), dtype=torch.bool)
+        shard.pack([good, bad], validate=f)
+        with pytest.raises(ValueError):
+            shard.check_flag(f)
+        with pytest.raises(ValueError):
+            shard.pack([bad])
+
+
+def test_rank_only_part_files_are_replaced(seq):
+    """--rank-only K (K > 0) writes its block into <log>.partK_* at offset 0
+    without truncating: stale longer part files from an earlier run must be
+    removed first."""
+    out = seq / "rankonly"
+    out.mkdir()
+    argv = ["-f", str(SEQ["n"]), "-s", f"{SEQ['W']}x{SEQ['H']}", "-q", str(SEQ["qp"]),
+            "-o", str(seq / "orig.csv"), "-r", str(seq / "recon.csv"), "-l", str(out / "log"),
+            "--gpus", "2", "--rank-only", "1"]
+    a = distrun.parse_args(argv)
+    a.shard_logs = True
+    table = torch.load(seq / "table.pt", weights_only=True)
+    pre = distrun.part_prefix(a.log, 1)
+    names = [os.path.basename(n) for n in __import__("vame.logs", fromlist=["x"]).log_names(pre)]
+    for n in names:  # stale, longer than any real part
+        (out / n).write_bytes(b"X" * 10_000_000)
+    distrun.run_rank(a, 2, 1, LookupEngine(a.W, a.H, table), torch.device("cpu"))
+    first = {n: (out / n).read_bytes() for n in names if (out / n).exists()}
+    assert first and all(b"X" * 64 not in v for v in first.values())
+    distrun.run_rank(a, 2, 1, LookupEngine(a.W, a.H, table), torch.device("cpu"))
+    assert {n: (out / n).read_bytes() for n in names if (out / n).exists()} == first
+
+
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("world", [2, 3])
 def test_shard_logs_byte_identical(seq, world):
@@ -203,10 +266,11 @@ def test_world_size_must_match_gpus(tmp_path):
 
 # ---- MI355X: the real rank processes with the HIP engine vs the vame CLI
 
-def run_distrun_gpu(tmp, W, H, n, qp, name, extra=()):
+def run_distrun_gpu(tmp, W, H, n, qp, name, extra=(), env_extra=None):
     out = tmp / name
     out.mkdir()
     env = dict(os.environ, VAME_DIST_BACKEND="gloo", PYTHONPATH=os.path.join(REPO, "vvc-affine-gpu_amd"))
+    env.update(env_extra or {})
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, "-m", "vame.distrun", "-f", str(n), "-s", f"{W}x{H}", "-q", str(qp),
@@ -242,6 +306,26 @@ def test_distrun_two_ranks_equals_cli(tmp_path, W, H, n):
         out, stdout = run_distrun_gpu(tmp_path, W, H, n, 32, name, ("--gpus", "2", *extra))
         assert len(compare_dirs(out, cli)) == 40, name
         assert "LOG_BYTES," in stdout and '"ranks": 2' in stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_distrun_forced_rccl_group_equals_cli(tmp_path):
+    """`python -m vame.distrun` in a one-rank RCCL process
+    group (VAME_FORCE_PG=1, backend nccl): init_process_group("nccl",
+    device_id=...), the records' dist.gather into rank 0 (rank 0's own, packed
+    on the GPU), all_gather_object of the timings -- and the 40 logs written
+    from the gathered slab equal the single-process CLI's byte for byte
+    (416x240, 7 POCs)."""
+    W, H, n = 416, 240, 7
+    orig, recon = synth_sequence(W, H, n, qp=32, seed=9)
+    write_csv(str(tmp_path / "orig.csv"), orig)
+    write_csv(str(tmp_path / "recon.csv"), recon)
+    cli = run_cli(tmp_path, W, H, n, 32)
+    out, stdout = run_distrun_gpu(tmp_path, W, H, n, 32, "rccl1", (),
+                                  {"VAME_DIST_BACKEND": "nccl", "VAME_FORCE_PG": "1"})
+    assert len(compare_dirs(out, cli)) == 40
+    assert '"ranks": 1' in stdout and "LOG_GATHER_TIME," in stdout
 
 
 class FakeEngine:

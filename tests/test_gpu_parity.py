@@ -134,42 +134,45 @@ def test_alignment_selection(engines, modes):
 REF_HARNESS = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle", "_ref", "ref_harness_hip")
 
 
-@pytest.mark.skipif(not os.path.exists(REF_HARNESS), reason="reference kernels not built")
-def test_live_reference_1080p(engines, tmp_path):
-    """The reference kernels themselves, run on this GPU, vs the HIP path at 1080p.
-
-    The reference hands gradients and equations between work-items through
-    global memory behind only a local barrier (affine.cl:487-514, 715-738), so
-    one of its runs can race.  As in the golden pipeline (make_golden.py
-    pack), the reference runs twice and its output counts only if both runs
-    agree bit for bit; if they do not, the HIP path is checked against the
-    oracle instead and the test reports the reference-side race as an xfail."""
-    from vame import synth
-    o, r = synth.synth_sequence(1920, 1080, 1, 32, seed=0xABCD)
-    lam = 78.949063
-    r[0].tofile(tmp_path / "ref.u16")
-    o[0].tofile(tmp_path / "cur.u16")
+def run_reference(tmp_path, W, H, lam, ref, cur, tag):
+    """The reference kernels themselves (oracle/_ref: affine.cl compiled
+    unmodified for gfx950, the host's four launches replayed by
+    ref_harness_hip) on one (POC, ref) pair, run twice (A/B).  Returns the two
+    runs' {PRED: (cost, cpmv[n, 6])}."""
     d = os.path.dirname(REF_HARNESS)
+    nctu = {(3840, 2160): 510, (1920, 1080): 135}[(W, H)]
+    ref.tofile(tmp_path / f"{tag}_ref.u16")
+    cur.tofile(tmp_path / f"{tag}_cur.u16")
     runs = []
-    for tag in ("A", "B"):
-        (tmp_path / f"jobs_{tag}.txt").write_text(
-            f"1920 1080 {lam!r} 0 {tmp_path / 'ref.u16'} {tmp_path / 'cur.u16'} {tmp_path / tag}\n")
+    for ab in ("A", "B"):
+        out = tmp_path / f"{tag}_{ab}"
+        (tmp_path / f"{tag}_jobs_{ab}.txt").write_text(
+            f"{W} {H} {lam!r} 0 {tmp_path / (tag + '_ref.u16')} {tmp_path / (tag + '_cur.u16')} {out}\n")
         subprocess.run([REF_HARNESS, os.path.join(d, "affine_2cp.co"), os.path.join(d, "affine_3cp.co"),
-                        str(tmp_path / f"jobs_{tag}.txt")], check=True, timeout=300, capture_output=True)
+                        str(tmp_path / f"{tag}_jobs_{ab}.txt")], check=True, timeout=300, capture_output=True)
         res = {}
         for name in MODES:
-            n = 135 * (201 if name.startswith("FULL") else 284)
-            raw = np.fromfile(tmp_path / f"{tag}_{name}.bin", np.uint8)
+            n = nctu * (201 if name.startswith("FULL") else 284)
+            raw = np.fromfile(f"{out}_{name}.bin", np.uint8)
             res[name] = (raw[:n * 8].view(np.int64), raw[n * 8:].view(np.int32).reshape(n, 7)[:, 1:])
         runs.append(res)
-    eng = engines(1920, 1080)
-    out = eng.affine_me_poc(dev(o[0]), [dev(r[0])], lam, modes=3)
+    return runs
+
+
+def check_vs_live_reference(runs, out, key_of, ref, cur, lam):
+    """HIP results `out[key_of(PRED)]` vs the reference's two runs.  The
+    reference hands gradients and equations between work-items through global
+    memory behind only a local barrier (affine.cl:487-514, 715-738), so one of
+    its runs can race: its output counts only if both runs agree bit for bit
+    (as in the golden pipeline, make_golden.py pack); if they do not, the HIP
+    path is checked against the oracle instead and the test reports the
+    reference-side race as an xfail."""
     racy = [name for name in MODES if not (np.array_equal(runs[0][name][0], runs[1][name][0])
                                            and np.array_equal(runs[0][name][1], runs[1][name][1]))]
     if racy:
-        want = O.affine_me_pair(r[0], o[0], lam)
-        for name, key in zip(MODES, ((0, 2), (0, 3), (1, 2), (1, 3))):
-            hc, hp = host(out[(0, name)])
+        want = O.affine_me_pair(ref, cur, lam)
+        for name, key in MODES.items():
+            hc, hp = host(out[key_of(name)])
             oc, op = want[key]
             np.testing.assert_array_equal(hc, oc, err_msg=name)
             np.testing.assert_array_equal(cp6(hp), oracle_cp6(op), err_msg=name)
@@ -177,9 +180,57 @@ def test_live_reference_1080p(engines, tmp_path):
                      f"715-738) on {racy}; the HIP path equals the oracle")
     for name in MODES:
         cost, cp = runs[0][name]
-        hc, hp = host(out[(0, name)])
+        hc, hp = host(out[key_of(name)])
         np.testing.assert_array_equal(hc, cost, err_msg=name)
         np.testing.assert_array_equal(cp6(hp), cp, err_msg=name)
+
+
+@pytest.mark.skipif(not os.path.exists(REF_HARNESS), reason="reference kernels not built")
+def test_live_reference_1080p(engines, tmp_path):
+    """The reference kernels themselves, run on this GPU, vs the HIP path at
+    1080p (POC 1, adjacent reference, the fused per-POC entry point)."""
+    from vame import synth
+    o, r = synth.synth_sequence(1920, 1080, 1, 32, seed=0xABCD)
+    lam = 78.949063
+    runs = run_reference(tmp_path, 1920, 1080, lam, r[0], o[0], "p1")
+    eng = engines(1920, 1080)
+    out = eng.affine_me_poc(dev(o[0]), [dev(r[0])], lam, modes=3)
+    check_vs_live_reference(runs, out, lambda name: (0, name), r[0], o[0], lam)
+
+
+# (W, H, QP, POC, refIdx) at the BASELINE configs' sizes (VERDICT r3 item 2):
+#   C4  3840x2160 POC 1 at the QP22 and QP37 lambdas (and their recon noise)
+#   C5  3840x2160 QP32 POC 239 refIdx 3: long-term reference POC 216, 23
+#       frames back -- the deepest motion of the sequence, many windows
+#       outside the staged tile (the mixed filter pass)
+#   C3  1920x1080 QP32 POC 26 refIdx 3: long-term reference POC 16
+LIVE_CASES = [(3840, 2160, 22, 1, 0), (3840, 2160, 37, 1, 0), (3840, 2160, 32, 239, 3),
+              (1920, 1080, 32, 26, 3)]
+
+
+@pytest.mark.skipif(not os.path.exists(REF_HARNESS), reason="reference kernels not built")
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("W,H,qp,poc,refidx", LIVE_CASES,
+                         ids=[f"{w}x{h}_qp{q}_poc{p}_ref{k}" for w, h, q, p, k in LIVE_CASES])
+def test_live_reference_configs(engines, tmp_path, W, H, qp, poc, refidx):
+    """The reference kernels vs the HIP batch path (vame_affine_me_batch, the
+    benchmarked entry point) on pairs of the C3 / C4 / C5 sequences, with the
+    reference's ring (main.cpp:591-707) and per-POC lambda (main.cpp:585):
+    all four PREDs, every cost and CPMV component, bit for bit."""
+    from vame import synth
+    from vame.hostlogic import lambda_for_poc, ref_list
+    rp = ref_list(poc)[refidx]
+    orig, recon = synth.synth_pocs(W, H, [poc], [rp], qp)
+    lam = lambda_for_poc(qp, poc)
+    runs = run_reference(tmp_path, W, H, lam, recon[rp], orig[poc], f"p{poc}r{refidx}")
+    eng = engines(W, H)
+    # the POC's whole ring in one batch, as the bench codes it; refIdx `refidx` is checked
+    refs = ref_list(poc)
+    others = synth.synth_pocs(W, H, [], [p for p in refs if p != rp], qp)[1]
+    d_refs = [dev(recon[p]) if p == rp else dev(others[p]) for p in refs]
+    job = (dev(orig[poc]), d_refs, lam, eng.alloc_poc(len(refs), 3))
+    eng.affine_me_batch([job], 3, 0)
+    check_vs_live_reference(runs, job[3], lambda name: (refidx, name), recon[rp], orig[poc], lam)
 
 
 PROF_CASES = [p for p in GOLDEN if any(k in p for k in ("qp32_poc1", "bigmotion", "extra1", "s832"))]

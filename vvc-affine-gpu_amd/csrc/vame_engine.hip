@@ -52,6 +52,9 @@ struct vame_ctx {
   bool prof = false;
   // VAME_JOIN_EACH=1: join the two streams after every launch of a batch
   bool joinEach = false;
+  // VAME_STREAMS=1: every kernel of a call on the caller's stream, all but the
+  // first without the AQL barrier bit (hipExtAnyOrderLaunch), no fork / join
+  int streams = 2;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];
   size_t evUsed[2] = {0, 0};
 };
@@ -355,7 +358,9 @@ int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool qua
   if (kps.empty()) return VAME_OK;
   const int mode = (kps[0].run2 ? 1 : 0) | (kps[0].run3 ? 2 : 0);  // the kernel instance (MODE)
   if (mode == 0) return VAME_OK;
-  const bool fork = bigItems && (quadFull || quadHalf);
+  const bool fork = c->streams != 1 && bigItems && (quadFull || quadHalf);
+  int issued = 0;  // VAME_STREAMS=1: kernels after a call's first may start before it ends
+  auto order_flag = [&]() { return c->streams == 1 && issued++ > 0 ? hipExtAnyOrderLaunch : 0; };
   hipStream_t sBig = stream, sQuad = stream;
   if (fork) {
     VAME_HIP(hipEventRecord(c->evFork, stream));
@@ -370,7 +375,7 @@ int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool qua
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 1, t0, t1));
     hipExtLaunchKernelGGL(kernel_for<true>(c->prof, mode), dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig,
-                          t0, t1, 0, kb);
+                          t0, t1, order_flag(), kb);
     VAME_HIP(hipGetLastError());
     return VAME_OK;
   };
@@ -382,23 +387,34 @@ int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool qua
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 0, t0, t1));
     hipExtLaunchKernelGGL(kernel_for<false>(c->prof, mode), dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad,
-                          t0, t1, 0, kq);
+                          t0, t1, order_flag(), kq);
     VAME_HIP(hipGetLastError());
     return VAME_OK;
   };
-  for (size_t k = 0; k < kps.size(); k++) {
-    if (bigItems) VAME_TRY(big(kps[k]));
-    if (quadFull || quadHalf) VAME_TRY(quad(kps[k]));
-    if (fork && (c->joinEach || k + 1 == kps.size())) {
-      VAME_HIP(hipEventRecord(c->evJoin, c->side));
-      VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
-      if (k + 1 < kps.size()) {  // VAME_JOIN_EACH: fork again for the next launch
-        VAME_HIP(hipEventRecord(c->evFork, stream));
-        VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
+  auto all = [&]() -> int {
+    for (size_t k = 0; k < kps.size(); k++) {
+      if (bigItems) VAME_TRY(big(kps[k]));
+      if (quadFull || quadHalf) VAME_TRY(quad(kps[k]));
+      if (fork && (c->joinEach || k + 1 == kps.size())) {
+        VAME_HIP(hipEventRecord(c->evJoin, c->side));
+        VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
+        if (k + 1 < kps.size()) {  // VAME_JOIN_EACH: fork again for the next launch
+          VAME_HIP(hipEventRecord(c->evFork, stream));
+          VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
+        }
       }
     }
+    return VAME_OK;
+  };
+  const int rc = all();
+  if (rc != VAME_OK && fork) {
+    // a launch failed after earlier quadrant kernels went to the side stream:
+    // order them before the caller's stream anyway, so the caller never frees
+    // or reuses result buffers they still write (best effort, the first error
+    // is the one reported)
+    if (hipEventRecord(c->evJoin, c->side) == hipSuccess) (void)hipStreamWaitEvent(stream, c->evJoin, 0);
   }
-  return VAME_OK;
+  return rc;
 }
 
 }  // namespace
@@ -465,6 +481,7 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   // tuning knobs of the block order (defaults measured on MI355X)
   const int xcdOrder = env_int("VAME_XCD_ORDER", 0);
   c->joinEach = env_int("VAME_JOIN_EACH", 0) != 0;
+  c->streams = env_int("VAME_STREAMS", 2) == 1 ? 1 : 2;
   c->groupCombos[0] = std::max(8, env_int("VAME_GROUP_COMBOS", 408));
   c->groupCombos[1] = std::max(8, env_int("VAME_GROUP_COMBOS_BIG", c->groupCombos[0]));
   for (int k = 0; k < 2 && e == hipSuccess; k++) {

@@ -210,15 +210,26 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
 
     # ---- who writes what: rank 0 appends to the final files as it goes; with
     # --shard-logs every other rank formats its block into host memory (a
-    # deferred writer) and places it into the same files at the end
-    writes_own = bool(a.log) and (rank == 0 or a.shard_logs)
+    # deferred writer) and places it into the same files at the end.  In a
+    # one-rank process group (VAME_FORCE_PG) rank 0's own records take the
+    # gather path too, so the collective and the writing from gathered slabs
+    # run on one GPU.
+    gather_path = bool(a.log) and not a.shard_logs and dist is not None
+    self_gather = gather_path and world == 1
+    writes_own = bool(a.log) and (rank == 0 or a.shard_logs) and not self_gather
     prefix = a.log if (rank == 0 or dist is not None) else part_prefix(a.log, rank)  # --rank-only K: parts
-    if a.log and rank == 0:
-        logs.remove_old(a.log)  # removeOldTraces (main.cpp:469)
-    writer = logs.LogWriter(prefix, W, H) if writes_own else None
+    if a.log and (rank == 0 or dist is None):
+        # removeOldTraces (main.cpp:469); a --rank-only K run's part files too:
+        # the deferred writer places its rows at offsets without truncating
+        logs.remove_old(prefix)
+    writer = logs.LogWriter(prefix, W, H) if (writes_own or (self_gather and rank == 0)) else None
     if writer is not None and rank > 0:
         writer.defer()
     slab_parts = []
+    # the compact-form check of the packed records, collected on the device and
+    # read once after the last launch (a per-launch read would stall the
+    # launching thread until that launch finished)
+    pack_bad = torch.zeros((), dtype=torch.bool, device=device)
 
     # ---- the writer thread: formats each launch's POCs once its copy landed
     slots = _HostSlots(2, cuda)
@@ -293,13 +304,16 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
                     ev.record(dnstream)
             work.put((ev, slot, batch, host))
         elif a.log:  # gather path: compact records stay on this GPU until the gather
-            slab_parts.append(shard.pack([j[3] for j in jobs], None, device, modes=modes))
+            slab_parts.append(shard.pack([j[3] for j in jobs], None, device, modes=modes,
+                                         validate=pack_bad))
     work.put(None)
     th.join()
     up_stop.set()
     up_th.join()
     if err:
         raise err[0]
+    if slab_parts:
+        shard.check_flag(pack_bad)
     if cuda:
         torch.cuda.synchronize()
         T["kernel_s"] = sum(x.elapsed_time(y) for x, y in spans) * 1e-3
@@ -307,7 +321,7 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
             T["gpu_gaps_s"] = spans[0][0].elapsed_time(spans[-1][1]) * 1e-3 - T["kernel_s"]
 
     # ---- the decision-log gather into rank 0 (default path)
-    if world > 1 and a.log and not a.shard_logs:
+    if gather_path and (world > 1 or self_gather):
         t = time.perf_counter()
         words = max(shard.slab_words(shard.block_layout(shard.pair_shard(a.frames, world, r), modes, n_cus))
                     for r in range(world))
@@ -321,7 +335,7 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
         T["gather_s"] = time.perf_counter() - t
         if rank == 0:
             t0 = time.perf_counter()
-            for r in range(1, world):
+            for r in range(0 if self_gather else 1, world):
                 o = 0
                 for poc, refs in shard.pair_shard(a.frames, world, r):
                     w = shard.poc_words(len(refs), modes, n_cus)

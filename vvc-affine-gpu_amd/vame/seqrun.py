@@ -97,11 +97,10 @@ class ShardRun:
     def gather(self):
         """The decision-record gather into rank 0: (slabs on rank 0 / None, bytes
         moved into rank 0)."""
+        import torch.distributed as dist
         slab = self.slab()
-        if self.world > 1:
-            import torch.distributed as dist
-            if dist.get_backend() == "gloo":  # CPU rehearsal of the RCCL path
-                slab = slab.cpu()
+        if dist.is_available() and dist.is_initialized() and dist.get_backend() == "gloo":
+            slab = slab.cpu()  # CPU rehearsal of the RCCL path
         slabs = shard.gather_to_root(slab, self.world, 0)
         return slabs, 4 * self.words * (self.world - 1)
 

@@ -116,12 +116,15 @@ def ncp_of(mode: str) -> int:
 
 
 def pack(results: list[dict], words: int | None = None, device=None, modes: int | None = None,
-         validate: bool = True) -> torch.Tensor:
+         validate: bool | torch.Tensor = True) -> torch.Tensor:
     """Concatenate the results of several POCs ({(ref, MODE): (cost int64[n],
     cpmv int32[n, 7])}, in POC order) into one int32 slab of compact records,
     zero padded to `words`.  With `modes`, every POC must hold exactly the
     keys `unpack` will expect for that mode mask; with `validate`, every record
-    must fit the compact form (0 <= cost < 2^31, 2-CP LB = (0, 0))."""
+    must fit the compact form (0 <= cost < 2^31, 2-CP LB = (0, 0)).  True
+    checks at once (a host read, which waits for the device); a bool tensor
+    instead collects the check into that flag on the device, with no wait, for
+    the caller to read once after its last launch (`check_flag`)."""
     parts = []
     for res in results:
         if modes is not None:
@@ -130,10 +133,14 @@ def pack(results: list[dict], words: int | None = None, device=None, modes: int 
                 raise ValueError(f"results {sorted(res)} do not match mode mask {modes}")
         for key in sorted(res, key=lambda k: (k[0], MODES.index(k[1]))):
             cost, cpmv = res[key]
-            if validate:  # the compact form drops 2-CP LB and the cost's upper half
+            if validate is not False:  # the compact form drops 2-CP LB and the cost's upper half
                 cp7 = cpmv.reshape(-1, 7)
-                if bool((cost < 0).any() or (cost >= 2**31).any()) or (
-                        ncp_of(key[1]) == 2 and bool(cp7[:, 5:].any())):
+                over = (cost < 0).any() | (cost >= 2**31).any()
+                if ncp_of(key[1]) == 2:
+                    over = over | cp7[:, 5:].any()
+                if isinstance(validate, torch.Tensor):
+                    validate.logical_or_(over.to(validate.device))
+                elif bool(over):
                     raise ValueError(f"records of {key} do not fit the compact form")
             parts.append(cost.reshape(-1).to(torch.int32))
             parts.append(cpmv.reshape(-1, 7)[:, 1:1 + 2 * ncp_of(key[1])].reshape(-1).to(torch.int32))
@@ -143,6 +150,13 @@ def pack(results: list[dict], words: int | None = None, device=None, modes: int 
             raise ValueError("slab larger than the agreed size")
         flat = torch.cat([flat, flat.new_zeros(words - flat.numel())])
     return flat
+
+
+def check_flag(flag: torch.Tensor) -> None:
+    """Raise if a deferred `pack(..., validate=flag)` check found a record
+    that does not fit the compact form (one host read)."""
+    if bool(flag.item()):
+        raise ValueError("decision records do not fit the compact form")
 
 
 def unpack(flat: torch.Tensor, layout: list[tuple[int, int, int]]) -> list[dict]:
@@ -182,9 +196,10 @@ def gather_to_root(slab: torch.Tensor, world: int, root: int = 0, group=None):
     """The one exchange step: every rank's equal-size slab to
     `root` (a rank of `group`, default the whole world) only (RCCL over xGMI on the GPU box: one ring-free gather into the
     root, 1/world of an all_gather's traffic).  Returns the list of slabs on
-    the root, None elsewhere."""
+    the root, None elsewhere.  A one-rank run without a process group keeps
+    its slab; with one (VAME_FORCE_PG) the slab goes through the collective."""
     import torch.distributed as dist
-    if world == 1:
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
         return [slab]
     rank = dist.get_rank(group)  # rank within the group; dist.gather's dst is a global rank
     dst = [torch.empty_like(slab) for _ in range(world)] if rank == root else None
