@@ -179,14 +179,17 @@ def main():
     elapsed = time.perf_counter() - t_start
     step_ms = sorted(step_ev[i].elapsed_time(step_ev[i + 1]) for i in range(args.steps))
     quad_ms, quad_n = eng.get_timing(0)
-    big_ms, big_n = eng.get_timing(1)
+    # the 128-class kernels (128x128 CUs: affine_me_ctu, class 1; 128x64 /
+    # 64x128 CUs: affine_me_half, class 2), timed in the timed steps only with
+    # VAME_BENCH_KTIMING=1, else on extra untimed steps after them
+    big_t = {k: eng.get_timing(k) for k in (1, 2)}
     big_on, big_steps = "timed steps", args.steps
-    if big_n == 0:  # the 128-class kernel's events, on extra untimed steps
+    if ktiming != 1:
         big_steps = min(args.steps, 20)
         eng.set_timing(True)
         for _ in range(big_steps):
             run.step()
-        big_ms, big_n = eng.get_timing(1)
+        big_t = {k: eng.get_timing(k) for k in (1, 2)}
         eng.get_timing(0)
         big_on = f"{big_steps} untimed steps after the timed ones"
     eng.set_timing(False)
@@ -228,8 +231,23 @@ def main():
     # roofline of the dominant kernel (quadrant work items, affine_me_quad)
     quad_bytes = acc["bytes_quad"] * run.pairs * args.steps
     achieved = quad_bytes / (quad_ms * 1e-3) / 1e9 if quad_ms > 0 else 0.0
-    big_bytes = acc["bytes_big"] * run.pairs * big_steps
-    big_achieved = big_bytes / (big_ms * 1e-3) / 1e9 if big_ms > 0 else 0.0
+    # per 128-class kernel: its dispatches' average and the algorithmic bytes
+    # it carries (VAME_HALF128=0: every 128-class CU in affine_me_ctu)
+    split = big_t[2][1] > 0
+    big_kernels = {}
+    for k, name, key in ((1, "affine_me_ctu", "bytes_ctu" if split else "bytes_big"),
+                         (2, "affine_me_half", "bytes_half")):
+        ms, n = big_t[k]
+        if n == 0:
+            continue
+        b = acc[key] * run.pairs * big_steps
+        ach = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        big_kernels[name] = {
+            "timed_on": big_on, "avg_launch_ms": ms / n, "launches": n, "alg_bytes_per_launch": b / n,
+            # algorithmic bytes over the dispatch's span, which runs beside the
+            # quadrant kernel and waits for CUs it frees: a residency span, not
+            # this kernel's efficiency (the whole step's figure is `step_frac`)
+            "resident_span_GBps": ach, "resident_span_frac": ach / HBM_PEAK_GBS}
     step_bytes = acc["bytes"] * run.pairs
     span_achieved = step_bytes / (span_ms * 1e-3) / 1e9 if span_ms > 0 else 0.0
     prof = load_profile(args.config, quad_ms / max(quad_n, 1))
@@ -290,11 +308,10 @@ def main():
                      "executed_pred_frac": prof.get("executed_pred_frac"),
                      # the kernel's real bound: VALU issue (rocprofv3 SQ counters, profiles/)
                      "valu": prof.get("valu"),
-                     "affine_me_ctu": {"achieved": big_achieved, "frac": big_achieved / HBM_PEAK_GBS,
-                                       "timed_on": big_on,
-                                       "avg_launch_ms": big_ms / max(big_n, 1),
-                                       "launches": big_n,
-                                       "alg_bytes_per_launch": big_bytes / max(big_n, 1)},
+                     # every kernel's algorithmic bytes over the whole timed step
+                     "step_frac": acc["bytes"] * run.pairs * args.steps / (elapsed * 1e9) / HBM_PEAK_GBS
+                     if elapsed > 0 else 0.0,
+                     **big_kernels,
                      "fused_poc_launch": {"achieved": span_achieved,
                                           "frac": span_achieved / HBM_PEAK_GBS,
                                           "avg_launch_ms": span_ms / max(span_n, 1),

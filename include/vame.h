@@ -108,7 +108,8 @@ int vame_set_prof(vame_ctx* ctx, int enable);
 /* Device-side kernel timing (the reference's per-PRED kernelExecutionTime,
  * main.cpp:856-866): when enabled, every kernel launch carries hipEvents in its
  * own dispatch on the stream it runs on.  kernel_class 0 = quadrant work items
- * (affine_me_quad), 1 = 128-class work items (affine_me_ctu).
+ * (affine_me_quad), 1 = 128x128 CUs (affine_me_ctu), 2 = 128x64 / 64x128 CUs
+ * (affine_me_half; with VAME_HALF128=0 at vame_create they run in class 1).
  * enable = 2 times the quadrant kernel only (its dispatches carry the events;
  * the 128-class launches run untimed).  vame_get_timing waits for the recorded
  * launches and returns their summed duration and count since the last reset. */

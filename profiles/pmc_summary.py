@@ -84,10 +84,11 @@ def timed_dispatches(d):
     K, W = line["steps"], line["warmup"]
     P = (line.get("prewarm") or {}).get("steps", 0)
     roof = line["roofline"]
-    launches = {"affine_me_quad": roof.get("launches"),
-                "affine_me_ctu": roof.get("affine_me_ctu", {}).get("launches")}
-    events = {"affine_me_quad": roof.get("avg_launch_ms"),
-              "affine_me_ctu": roof.get("affine_me_ctu", {}).get("avg_launch_ms")}
+    launches = {"affine_me_quad": roof.get("launches")}
+    events = {"affine_me_quad": roof.get("avg_launch_ms")}
+    for k in ("affine_me_ctu", "affine_me_half"):  # the 128-class kernels (timed on their own steps)
+        launches[k] = roof.get(k, {}).get("launches")
+        events[k] = roof.get(k, {}).get("avg_launch_ms")
     out = {}
     for k, L in launches.items():
         if not L or L % K or k not in per:

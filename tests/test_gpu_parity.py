@@ -407,6 +407,41 @@ def test_property_translation_1080p(engines, d):
     assert n > 1000 and frac >= 0.75, (frac, n)
 
 
+@pytest.mark.parametrize("env", [{"VAME_HALF128": "0"}, {"VAME_STREAMS": "1"},
+                                 {"VAME_STREAMS": "1", "VAME_HALF128": "0"}],
+                         ids=["ctu1024_packing", "one_stream", "one_stream_ctu1024"])
+def test_launch_structure_variants(env, monkeypatch):
+    """The engine's launch-structure knobs (read at vame_create) change only
+    where the work runs: VAME_HALF128=0 puts the 128x64 / 64x128 CUs back into
+    the 1024-thread CTU items (two CUs per workgroup) instead of one 512-thread
+    affine_me_half workgroup each; VAME_STREAMS=1 issues every kernel of a call
+    on the caller's stream (all but the first without the AQL barrier bit)
+    instead of forking a side stream.  A 1080p POC with 2 refs (2+3 CP) and a
+    2-CP-only POC give the default context's results bit for bit, and the
+    default equals the oracle on one pair."""
+    from vame.engine import Engine
+    from vame import synth
+    o, r = synth.synth_sequence(1920, 1080, 2, 32, seed=0x0DE6)
+    cur, refs = dev(o[1]), [dev(r[1]), dev(r[0])]
+    base = Engine(1920, 1080, 0)
+    want = {m: base.affine_me_poc(cur, refs, 70.335619, modes=m) for m in (3, 1)}
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    eng = Engine(1920, 1080, 0)
+    got = {m: eng.affine_me_poc(cur, refs, 70.335619, modes=m) for m in (3, 1)}
+    torch.cuda.synchronize()
+    for m in want:
+        for k in want[m]:
+            assert torch.equal(want[m][k][0], got[m][k][0]) and torch.equal(want[m][k][1], got[m][k][1]), (m, k)
+    oracle = O.affine_me_pair(r[0], o[1], 70.335619)
+    for name, key in MODES.items():
+        hc, hp = host(want[3][(1, name)])
+        np.testing.assert_array_equal(hc, oracle[key][0], err_msg=name)
+        np.testing.assert_array_equal(cp6(hp), oracle_cp6(oracle[key][1]), err_msg=name)
+    eng.close()
+    base.close()
+
+
 @pytest.mark.parametrize("combos,order", [(16, 0), (24, 1), (64, 2), (408, 4), (100, 3)])
 def test_block_order_variants(combos, order, monkeypatch):
     """The block order's knobs (VAME_GROUP_COMBOS / _BIG, VAME_XCD_ORDER, read

@@ -39,7 +39,8 @@ struct vame_ctx {
   // device-resident work-item templates: [quadFull | quadHalf] and big (FULL 128-class)
   Item* dQuad = nullptr;
   Item* dBig = nullptr;
-  int nQuadFull = 0, nQuadHalf = 0, nBig = 0;
+  Item* dHalf = nullptr;  // affine_me_half items: one 128x64 / 64x128 CU each (VAME_HALF128, default on)
+  int nQuadFull = 0, nQuadHalf = 0, nBig = 0, nHalf = 0;
   // block order (block_grid), per kernel class (0 quadrant, 1 128-class):
   // slot -> CTU table, group size, CTU chunks, slots per (pair, chunk)
   int32_t* dOrder[2] = {nullptr, nullptr};
@@ -47,6 +48,7 @@ struct vame_ctx {
   hipStream_t side = nullptr;   // second stream: 128-class items run beside the quadrant items
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   // optional per-kernel timing: (start, end) event pairs per kernel class
+  // (0 quadrant, 1 128x128 CTU, 2 128x64 / 64x128 CUs)
   int timing = 0;
   // PROF on (vame_set_prof): the *_prof kernels
   bool prof = false;
@@ -55,8 +57,8 @@ struct vame_ctx {
   // VAME_STREAMS=1: every kernel of a call on the caller's stream, all but the
   // first without the AQL barrier bit (hipExtAnyOrderLaunch), no fork / join
   int streams = 2;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];
-  size_t evUsed[2] = {0, 0};
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[3];
+  size_t evUsed[3] = {0, 0, 0};
 };
 
 namespace {
@@ -156,19 +158,32 @@ void pack_autonomous(int qx, int qy, std::vector<CuDesc> cus, std::vector<Item>&
 }
 
 // Work-item templates (identical for every CTU):
-//   big      : FULL 128x128 / 128x64 / 64x128 groups, whole CTU, cooperative
+//   big      : FULL 128x128 group (and, without `half`, the 128x64 / 64x128
+//              groups), whole CTU, cooperative
+//   half     : with `half`, each 128x64 / 64x128 CU alone, its own region
+//              (affine_me_half, 512 threads)
 //   quadFull : FULL groups <= 64x64 per 64x64 quadrant: 64x64 / 64x32 / 32x64
 //              cooperative (one item per group), the rest autonomous
 //   quadHalf : HALF groups per quadrant (no HALF CU crosses a quadrant):
 //              64x32 + 32x64 cooperative, the rest autonomous
-void build_templates(std::vector<Item>& big, std::vector<Item>& quadFull,
-                     std::vector<Item>& quadHalf) {
+void build_templates(std::vector<Item>& big, std::vector<Item>& halfItems, std::vector<Item>& quadFull,
+                     std::vector<Item>& quadHalf, bool half) {
   for (int g = 0; g < kFullGroups; g++) {
     const int w = kFullW[g], h = kFullH[g], n = (kCtu * kCtu) / (w * h), cols = kCtu / w;
     if (w == 128 || h == 128) {
       std::vector<CuDesc> c;
       for (int k = 0; k < n; k++) c.push_back({(k % cols) * w, (k / cols) * h, w, h, 0, kFullStride[g] + k});
-      if (!((VAME_ABLATE & 256) && w != h)) big.push_back(make_coop_item(0, 0, c, Cfg<128>::THREADS));
+      if ((VAME_ABLATE & 256) && w != h) continue;
+      if (half && w != h) {
+        for (auto& cu : c) {  // one CU per item, the region = the CU
+          Item it = make_coop_item(cu.x, cu.y, {cu}, Cfg<kKindHalf>::THREADS);
+          it.rw = (int16_t)w;
+          it.rh = (int16_t)h;
+          halfItems.push_back(it);
+        }
+      } else {
+        big.push_back(make_coop_item(0, 0, c, Cfg<kKindCtu>::THREADS));
+      }
     }
   }
   for (int q = 0; q < 4; q++) {
@@ -184,7 +199,7 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& quadFull,
         if (inq(x, y)) c.push_back({x, y, w, h, 0, kFullStride[g] + k});
       }
       if (w * h / 16 > 64)
-        quadFull.push_back(make_coop_item(qx, qy, c, Cfg<64>::THREADS));
+        quadFull.push_back(make_coop_item(qx, qy, c, Cfg<kKindQuad>::THREADS));
       else
         small.insert(small.end(), c.begin(), c.end());
     }
@@ -199,7 +214,7 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& quadFull,
         const CuDesc c{x, y, kHalfW[g], kHalfH[g], 1, kHalfStride[g] + k};
         (nsb_of(c) > 64 ? bigHalf : small).push_back(c);
       }
-    if (!bigHalf.empty()) quadHalf.push_back(make_coop_item(qx, qy, bigHalf, Cfg<64>::THREADS));
+    if (!bigHalf.empty()) quadHalf.push_back(make_coop_item(qx, qy, bigHalf, Cfg<kKindQuad>::THREADS));
     pack_autonomous(qx, qy, small, quadHalf);
   }
 }
@@ -329,11 +344,14 @@ int env_int(const char* name, int dflt) {
 // The kernel instance of a launch mode (vame_kernel.h MODE: 1 = 2-CP only,
 // 2 = 3-CP only, 3 = 2-CP then 3-CP).
 using KernelFn = void (*)(KParams);
-template <bool BIG>
+template <int KIND>
 KernelFn kernel_for(bool prof, int mode) {
-  if constexpr (BIG) {
+  if constexpr (KIND == kKindCtu) {
     if (prof) return mode == 1 ? affine_me_ctu_prof<1> : mode == 2 ? affine_me_ctu_prof<2> : affine_me_ctu_prof<3>;
     return mode == 1 ? affine_me_ctu<1> : mode == 2 ? affine_me_ctu<2> : affine_me_ctu<3>;
+  } else if constexpr (KIND == kKindHalf) {
+    if (prof) return mode == 1 ? affine_me_half_prof<1> : mode == 2 ? affine_me_half_prof<2> : affine_me_half_prof<3>;
+    return mode == 1 ? affine_me_half<1> : mode == 2 ? affine_me_half<2> : affine_me_half<3>;
   } else {
     if (prof) return mode == 1 ? affine_me_quad_prof<1> : mode == 2 ? affine_me_quad_prof<2> : affine_me_quad_prof<3>;
     return mode == 1 ? affine_me_quad<1> : mode == 2 ? affine_me_quad<2> : affine_me_quad<3>;
@@ -374,8 +392,20 @@ int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool qua
     const unsigned grid = block_grid(c, 1, kb);
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 1, t0, t1));
-    hipExtLaunchKernelGGL(kernel_for<true>(c->prof, mode), dim3(grid), dim3(Cfg<128>::THREADS), 0, sBig,
-                          t0, t1, order_flag(), kb);
+    hipExtLaunchKernelGGL(kernel_for<kKindCtu>(c->prof, mode), dim3(grid), dim3(Cfg<kKindCtu>::THREADS), 0,
+                          sBig, t0, t1, order_flag(), kb);
+    VAME_HIP(hipGetLastError());
+    return VAME_OK;
+  };
+  auto half = [&](const KParams& kp) -> int {  // after the 128x128 items, on their stream
+    KParams kh = kp;
+    kh.items = c->dHalf;
+    kh.nItems = c->nHalf;
+    const unsigned grid = block_grid(c, 1, kh);
+    hipEvent_t t0, t1;
+    VAME_TRY(time_events(c, 2, t0, t1));
+    hipExtLaunchKernelGGL(kernel_for<kKindHalf>(c->prof, mode), dim3(grid), dim3(Cfg<kKindHalf>::THREADS), 0,
+                          sBig, t0, t1, order_flag(), kh);
     VAME_HIP(hipGetLastError());
     return VAME_OK;
   };
@@ -386,14 +416,15 @@ int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool qua
     const unsigned grid = block_grid(c, 0, kq);
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 0, t0, t1));
-    hipExtLaunchKernelGGL(kernel_for<false>(c->prof, mode), dim3(grid), dim3(Cfg<64>::THREADS), 0, sQuad,
-                          t0, t1, order_flag(), kq);
+    hipExtLaunchKernelGGL(kernel_for<kKindQuad>(c->prof, mode), dim3(grid), dim3(Cfg<kKindQuad>::THREADS), 0,
+                          sQuad, t0, t1, order_flag(), kq);
     VAME_HIP(hipGetLastError());
     return VAME_OK;
   };
   auto all = [&]() -> int {
     for (size_t k = 0; k < kps.size(); k++) {
-      if (bigItems) VAME_TRY(big(kps[k]));
+      if (bigItems && c->nBig) VAME_TRY(big(kps[k]));
+      if (bigItems && c->nHalf) VAME_TRY(half(kps[k]));
       if (quadFull || quadHalf) VAME_TRY(quad(kps[k]));
       if (fork && (c->joinEach || k + 1 == kps.size())) {
         VAME_HIP(hipEventRecord(c->evJoin, c->side));
@@ -464,8 +495,8 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (device < 0 || device >= ndev) return VAME_E_INVALID;
   DeviceGuard guard(device);
   VAME_HIP(guard.err);
-  std::vector<Item> big, qf, qh;
-  build_templates(big, qf, qh);
+  std::vector<Item> big, hf, qf, qh;
+  build_templates(big, hf, qf, qh, env_int("VAME_HALF128", 1) != 0);
   vame_ctx* c = new vame_ctx();
   c->device = device;
   c->W = width;
@@ -473,6 +504,7 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   c->nCtus = nCtus;
   c->ctusPerRow = (width + kCtu - 1) / kCtu;  // T8: integer ceil
   c->nBig = (int)big.size();
+  c->nHalf = (int)hf.size();
   c->nQuadFull = (int)qf.size();
   c->nQuadHalf = (int)qh.size();
   std::vector<Item> quad(qf);
@@ -494,6 +526,9 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (e == hipSuccess) e = hipMalloc(&c->dBig, big.size() * sizeof(Item));
   if (e == hipSuccess) e = hipMemcpy(c->dQuad, quad.data(), quad.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->dBig, big.data(), big.size() * sizeof(Item), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !hf.empty()) e = hipMalloc(&c->dHalf, hf.size() * sizeof(Item));
+  if (e == hipSuccess && !hf.empty())
+    e = hipMemcpy(c->dHalf, hf.data(), hf.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming);
@@ -511,12 +546,13 @@ void vame_destroy(vame_ctx* c) {
   DeviceGuard guard(c->device);
   if (c->dQuad) (void)hipFree(c->dQuad);
   if (c->dBig) (void)hipFree(c->dBig);
+  if (c->dHalf) (void)hipFree(c->dHalf);
   for (int k = 0; k < 2; k++)
     if (c->dOrder[k]) (void)hipFree(c->dOrder[k]);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->evFork) (void)hipEventDestroy(c->evFork);
   if (c->evJoin) (void)hipEventDestroy(c->evJoin);
-  for (int k = 0; k < 2; k++)
+  for (int k = 0; k < 3; k++)
     for (auto& e : c->ev[k]) {
       (void)hipEventDestroy(e.first);
       (void)hipEventDestroy(e.second);
@@ -621,13 +657,14 @@ int vame_set_prof(vame_ctx* c, int enable) {
 
 int vame_set_timing(vame_ctx* c, int enable) {
   if (!c) return VAME_E_INVALID;
-  c->timing = enable == 2 ? 1 : enable != 0 ? 3 : 0;  // kernel classes timed (bit 0 quadrant, bit 1 128-class)
-  c->evUsed[0] = c->evUsed[1] = 0;
+  // kernel classes timed: bit 0 quadrant, bit 1 128x128, bit 2 128x64 / 64x128
+  c->timing = enable == 2 ? 1 : enable != 0 ? 7 : 0;
+  c->evUsed[0] = c->evUsed[1] = c->evUsed[2] = 0;
   return VAME_OK;
 }
 
 int vame_get_timing(vame_ctx* c, int cls, double* total_ms, int* launches, int reset) {
-  if (!c || cls < 0 || cls > 1 || !total_ms || !launches) return VAME_E_INVALID;
+  if (!c || cls < 0 || cls > 2 || !total_ms || !launches) return VAME_E_INVALID;
   DeviceGuard guard(c->device);
   VAME_HIP(guard.err);
   double t = 0;

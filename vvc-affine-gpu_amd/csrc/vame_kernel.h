@@ -71,7 +71,7 @@ struct Item {
   int16_t coop;     // 1: cooperative (CUs span waves, all CUs of one size)
   int16_t nWaves;   // autonomous: waves holding CUs
   int16_t logL;     // cooperative: log2 lanes per CU (>= 6)
-  int16_t pad0, pad1;
+  int16_t rw, rh;   // affine_me_half items: the region's extent (the CU's); 0 elsewhere
   WaveDesc wave[kMaxWaves];
   CuSlot cu[kMaxCu];
 };
@@ -755,7 +755,7 @@ __device__ __forceinline__ void prof_refine(const int (&acc)[4][4], const MvFiel
 // the gradient step, and so do the original samples (O[r]).
 template <int TILE, int TP, bool PROF, bool FORCE_TILE = false>
 __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, const Geo& g,
-                                          const uint16_t* s_tile, int tx0, int ty0,
+                                          const uint16_t* s_tile, int tx0, int ty0, int tmx, int tmy,
                                           const uint16_t* __restrict__ ref,
                                           const uint16_t* __restrict__ cur, int W, int H,
                                           const uint4* s_coef, uint2 (&P)[4], uint2 (&O)[4],
@@ -778,17 +778,18 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   const int wx = g.x + sx + ix - 2, wy = g.y + sy + iy - 2;  // window origin (frame)
   int tx = wx - tx0, ty = wy - ty0;
   if ((VAME_ABLATE & 512) || FORCE_TILE) {  // timing-only: every window read from the tile (wrong results)
-    tx = clampi(tx, 0, TILE - 9);
-    ty = clampi(ty, 0, TILE - 9);
+    tx = clampi(tx, 0, tmx);
+    ty = clampi(ty, 0, tmy);
   }
-  const bool inTile = (unsigned)tx <= (unsigned)(TILE - 9) && (unsigned)ty <= (unsigned)(TILE - 9);
+  // tmx / tmy: the largest window origin inside the staged tile (its extent - 9)
+  const bool inTile = (unsigned)tx <= (unsigned)tmx && (unsigned)ty <= (unsigned)tmy;
   outside = !inTile;
 #if VAME_COUNT_PRED
   {  // instrumentation: outside windows that a 4 / 8 / 16 px wider margin would hold
 #pragma unroll
     for (int e = 0; e < 3; e++) {
       const int x = 4 << e;
-      const bool in = (unsigned)(tx + x) <= (unsigned)(TILE - 9 + 2 * x) && (unsigned)(ty + x) <= (unsigned)(TILE - 9 + 2 * x);
+      const bool in = (unsigned)(tx + x) <= (unsigned)(tmx + 2 * x) && (unsigned)(ty + x) <= (unsigned)(tmy + 2 * x);
       const unsigned long long m = __builtin_amdgcn_ballot_w64(!inTile && in);
       if (m && __lane_id() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
         atomicAdd(&g_pred_count[6 + 3 * (TILE > 100) + e], (unsigned long long)__popcll(m));
@@ -1140,16 +1141,25 @@ struct CuState {
   int32_t pad;
 };
 
-template <int REGION>
+// Work-item classes (kernels): 0 affine_me_quad -- a 64x64 quadrant, 256
+// threads; 1 affine_me_ctu -- a whole 128x128 CTU, 1024 threads; 2
+// affine_me_half -- ONE 128x64 or 64x128 CU, 512 threads (two workgroups per
+// CU: one's single-wave solve overlaps the other's prediction), its tile
+// staged over the CU's extent only (160 x 96 or 96 x 160 of the square
+// storage).
+enum { kKindQuad = 0, kKindCtu = 1, kKindHalf = 2 };
+template <int KIND>
 struct Cfg {
-  static constexpr int THREADS = REGION == 128 ? 1024 : 256;  // workgroup size = sub-blocks
+  static constexpr int REGION = KIND == kKindQuad ? 64 : 128;  // largest region edge
+  static constexpr int THREADS = KIND == kKindQuad ? 256 : KIND == kKindCtu ? 1024 : 512;  // = sub-blocks
+  static constexpr int MAXCU = KIND == kKindHalf ? 1 : kMaxCu;  // CU slots per item
   static constexpr int MARGIN = 16;                     // reference-tile margin (samples)
   static constexpr int TILE = REGION + 2 * MARGIN;      // tile edge (samples)
   // tile pitch (samples) == 8 (mod 16): the window rows of sub-blocks 4 rows
   // apart land 16 banks apart (2-way at most for the packed-pair reads)
   static constexpr int TP = (TILE + 7) / 16 * 16 + 8;
   static constexpr int TILE_ELEMS = TILE * TP + 16;
-  static constexpr int NSB = REGION * REGION / 16;      // sub-blocks per work item (max)
+  static constexpr int NSB = THREADS;                   // sub-blocks per work item (max)
 };
 
 // Value i of a sub-block's contribution to its CU's normal equations
@@ -1453,10 +1463,11 @@ __device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v
 
 // MODE (one kernel per launch mode, so each holds only the pass copies it
 // runs): 1 = 2-CP only, 2 = 3-CP only (seeds from p.prev), 3 = 2-CP then 3-CP.
-template <int REGION, bool PROF, int MODE>
+template <int KIND, bool PROF, int MODE>
 __device__ __forceinline__ void affine_me_body(const KParams& p) {
   constexpr bool run2 = (MODE & 1) != 0, run3 = (MODE & 2) != 0;
-  using C = Cfg<REGION>;
+  using C = Cfg<KIND>;
+  constexpr int REGION = C::REGION;  // instrumentation slots: 128 = the 128-class kernels
   __shared__ __attribute__((aligned(16))) uint16_t s_tile[C::TILE_ELEMS];
   static_assert((C::TP * 2) % 16 == 0 && C::TILE % 8 == 0, "16-byte tile rows");
   __shared__ uint2 s_top[C::NSB];  // row 0 of every sub-block's prediction (packed pairs)
@@ -1464,12 +1475,12 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   // the five gradient sums of every sub-block at its CU's best 2-CP iteration
   // (3-CP seed reuse, see the 3-CP init)
   __shared__ int s_bestS[5][C::NSB];
-  __shared__ __attribute__((aligned(16))) long long s_val[kMaxCu][kNumMom];
-  __shared__ double s_mat[kMaxCu][42];  // per CU: N x (N + 1) system, N <= 6
+  __shared__ __attribute__((aligned(16))) long long s_val[C::MAXCU][kNumMom];
+  __shared__ double s_mat[C::MAXCU][42];  // per CU: N x (N + 1) system, N <= 6
   __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
   __shared__ uint8_t s_eqmap[80];
-  __shared__ CuState s_st[kMaxCu];
-  __shared__ CuSlot s_cu[kMaxCu];
+  __shared__ CuState s_st[C::MAXCU];
+  __shared__ CuSlot s_cu[C::MAXCU];
   __shared__ WaveDesc s_wave[kMaxWaves];
   __shared__ int s_hdr[4];
   __shared__ long long s_dup[(VAME_DUP & 4) ? kNumMom : 1];
@@ -1514,9 +1525,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   // descriptor loads, and one barrier publishes both
   const int tx0 = ctuX + (int)it->rx - C::MARGIN, ty0 = ctuY + (int)it->ry - C::MARGIN;  // tile origin
   const bool regionOut = tx0 + C::MARGIN >= W || ty0 + C::MARGIN >= H;
-  constexpr int CPR = C::TILE / 8;  // chunks per tile row
-  constexpr int NCH = C::TILE * CPR;
-  constexpr int PER = (NCH + C::THREADS - 1) / C::THREADS;
+  // the staged extent: the whole square tile, or (affine_me_half) the CU's
+  // region + margin, a 160 x 96 or 96 x 160 part of the square storage
+  const int tileW = KIND == kKindHalf ? (int)it->rw + 2 * C::MARGIN : C::TILE;
+  const int tileH = KIND == kKindHalf ? (int)it->rh + 2 * C::MARGIN : C::TILE;
+  const int CPR = tileW / 8;  // chunks per tile row
+  const int NCH = tileH * CPR;
+  constexpr int PER = (C::TILE * (C::TILE / 8) + C::THREADS - 1) / C::THREADS;
   uint4 tv[PER];
   if constexpr ((VAME_DUP & 64) != 0) {  // timing-only: one extra staging round trip
     if (!regionOut) {
@@ -1555,12 +1570,12 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       }
     }
   }
-  if (tid < kMaxCu) s_cu[tid] = it->cu[tid];
+  if (tid < C::MAXCU) s_cu[tid] = it->cu[tid];
   if (tid < kMaxWaves) s_wave[tid] = it->wave[tid];
   if (tid < 48) s_coef[tid] = reinterpret_cast<const uint4*>(&kCoefTab)[tid];
   if (tid < 80) s_eqmap[tid] = kEqMap.v[tid];
   if (tid == 0) s_hdr[0] = it->nCu | (it->coop << 8) | (it->nWaves << 16) | (it->logL << 24);
-  for (int i = tid; i < kMaxCu * kNumMom; i += C::THREADS) (&s_val[0][0])[i] = 0;
+  for (int i = tid; i < C::MAXCU * kNumMom; i += C::THREADS) (&s_val[0][0])[i] = 0;
   PH_INIT
   if (!regionOut) {
 #pragma unroll
@@ -1727,7 +1742,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
         bool outside;
         const int satdLane = predict_sb<C::TILE, C::TP, PROF, (VAME_ABLATE & 1024) != 0 && ncp == 3>(
-            f, sxp, syp, gp, s_tile, tx0, ty0, ref, cur, W, H, s_coef, Pr, Og, outside);
+            f, sxp, syp, gp, s_tile, tx0, ty0, tileW - 9, tileH - 9, ref, cur, W, H, s_coef, Pr, Og, outside);
 #if VAME_COUNT_PRED
         {  // instrumentation: windows outside the tile, per kernel and pass, one atomic per wave
           const unsigned long long out = __builtin_amdgcn_ballot_w64(outside);
@@ -1740,8 +1755,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           opaque(f2.bx);
           uint2 P2[4], O2[4];
           bool out2;
-          int s2 = predict_sb<C::TILE, C::TP, PROF>(f2, sxp, syp, gp, s_tile, tx0, ty0, ref, cur, W, H,
-                                              s_coef, P2, O2, out2);
+          int s2 = predict_sb<C::TILE, C::TP, PROF>(f2, sxp, syp, gp, s_tile, tx0, ty0, tileW - 9, tileH - 9,
+                                                    ref, cur, W, H, s_coef, P2, O2, out2);
           s2 += (int)(P2[0].x ^ P2[3].y ^ O2[1].x);
           asm volatile("" ::"v"(s2));
         }
@@ -1996,19 +2011,29 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 template <int MODE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad(
     KParams p) {
-  affine_me_body<64, false, MODE>(p);
+  affine_me_body<kKindQuad, false, MODE>(p);
 }
 // 128-class items: one 1024-thread workgroup per CU (~100 KB of LDS), one lane
 // per sub-block of a 128x128 CU.
 template <int MODE>
-__global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_body<128, false, MODE>(p); }
+__global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_body<kKindCtu, false, MODE>(p); }
+// One 128x64 / 64x128 CU per 512-thread workgroup, two per CU (~74 KB of LDS
+// each): 128 VGPRs so both fit.
+template <int MODE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_half(KParams p) {
+  affine_me_body<kKindHalf, false, MODE>(p);
+}
 // The same with PROF (vame_set_prof).
 template <int MODE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad_prof(
     KParams p) {
-  affine_me_body<64, true, MODE>(p);
+  affine_me_body<kKindQuad, true, MODE>(p);
 }
 template <int MODE>
-__global__ __launch_bounds__(1024) void affine_me_ctu_prof(KParams p) { affine_me_body<128, true, MODE>(p); }
+__global__ __launch_bounds__(1024) void affine_me_ctu_prof(KParams p) { affine_me_body<kKindCtu, true, MODE>(p); }
+template <int MODE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_half_prof(KParams p) {
+  affine_me_body<kKindHalf, true, MODE>(p);
+}
 
 }  // namespace vame

@@ -70,7 +70,8 @@ class Engine:
         check(lib().vame_set_timing(self._h, int(enable)))
 
     def get_timing(self, kernel_class: int, reset: bool = True):
-        """(total_ms, launches) of kernel class 0 (quadrant items) / 1 (128-class items)."""
+        """(total_ms, launches) of kernel class 0 (quadrant items, affine_me_quad) /
+        1 (128x128 CUs, affine_me_ctu) / 2 (128x64 and 64x128 CUs, affine_me_half)."""
         t, n = ctypes.c_double(), ctypes.c_int()
         check(lib().vame_get_timing(self._h, kernel_class, ctypes.byref(t), ctypes.byref(n), int(reset)))
         return t.value, n.value

@@ -34,9 +34,11 @@ def cu_inventory(W: int, H: int):
 
 def pair_accounting(W: int, H: int, ncps=(2,), extra: int = 0):
     """Per (POC, ref) pair: rows, in-frame rows, and B_alg split by kernel class
-    ('quad' = affine_me_quad items, 'big' = affine_me_ctu items)."""
-    acc = {"rows": 0, "rows_inframe": 0, "bytes_quad": 0, "bytes_big": 0, "sb_pred": 0,
-           "sb_pred_quad": 0, "sb_pred_big": 0}
+    ('quad' = affine_me_quad items, 'big' = the 128-class CUs: 'ctu' = the
+    128x128 CUs of affine_me_ctu, 'half' = the 128x64 / 64x128 CUs of
+    affine_me_half)."""
+    acc = {"rows": 0, "rows_inframe": 0, "bytes_quad": 0, "bytes_big": 0, "bytes_ctu": 0,
+           "bytes_half": 0, "sb_pred": 0, "sb_pred_quad": 0, "sb_pred_big": 0}
     inv = cu_inventory(W, H)
     for ncp in ncps:
         npred = N_PRED[ncp] + extra
@@ -50,5 +52,7 @@ def pair_accounting(W: int, H: int, ncps=(2,), extra: int = 0):
                 acc["sb_pred"] += npred * nsb
                 acc["sb_pred_big" if big else "sb_pred_quad"] += npred * nsb
             acc["bytes_big" if big else "bytes_quad"] += b
+            if big:
+                acc["bytes_ctu" if w == h else "bytes_half"] += b
     acc["bytes"] = acc["bytes_quad"] + acc["bytes_big"]
     return acc
