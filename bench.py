@@ -302,6 +302,12 @@ def main():
                      # the same kernel's average under rocprofv3 over the timed
                      # dispatches of a traced run of this config (profiles/)
                      "rocprof_avg_ms": prof.get("rocprof_avg_ms"),
+                     # the committed profile the rocprof / counter fields come
+                     # from, the workload it was taken on, and whether that is
+                     # this line's workload
+                     "profile": prof.get("profile"),
+                     "profiled_workload": prof.get("profiled_workload"),
+                     "profile_matches_workload": profile_matches(prof, cfg, run, world, args.rank_only),
                      "alg_bytes_per_launch": quad_bytes / max(quad_n, 1),
                      # fraction of the algorithmic sub-block predictions the exact
                      # early exit actually runs (instrumented build, profiles/)
@@ -355,6 +361,19 @@ def native_record() -> dict:
     return rec
 
 
+def profile_matches(prof: dict, cfg: dict, run, world: int, rank_only) -> bool | None:
+    """Whether the committed profile was taken on this line's workload (same
+    resolution, QP, modes, pairs per step and rank block), so that its
+    rocprof average and counters describe the launches this line times."""
+    pw = prof.get("profiled_workload")
+    if not pw:
+        return None
+    ro = {"rank": rank_only, "of": world} if rank_only is not None else None
+    return (pw.get("resolution") == f"{cfg['W']}x{cfg['H']}" and pw.get("qp") == cfg["qp"]
+            and pw.get("modes") == ("2cp+3cp" if cfg["modes"] & 2 else "2cp")
+            and pw.get("pairs_per_step_rank0") == run.pairs and pw.get("rank_only") == ro)
+
+
 def load_profile(config: str, avg_launch_ms: float) -> dict:
     """Counter-derived figures for the quadrant kernel from the committed
     profile of this config (profiles/pmc_<config>.json, written by
@@ -369,7 +388,9 @@ def load_profile(config: str, avg_launch_ms: float) -> dict:
     p = json.load(open(path))
     out = {"traffic": p.get("quad_hbm_bytes_per_launch"),
            "executed_pred_frac": p.get("executed_pred_frac"),
-           "rocprof_avg_ms": p.get("quad_timed_avg_ms_rocprof")}
+           "rocprof_avg_ms": p.get("quad_timed_avg_ms_rocprof"),
+           "profiled_workload": p.get("profiled_workload"),
+           "profile": os.path.relpath(path, REPO)}
     sq = p.get("quad_sq")
     if sq and avg_launch_ms > 0:
         clk = sq["clock_ghz"]

@@ -76,7 +76,7 @@ def timed_dispatches(d):
                 line = json.loads(l)
     path = os.path.join(d, "trace", "run_kernel_trace.csv")
     if line is None or not os.path.exists(path):
-        return {}, {}
+        return {}, {}, None
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     per = defaultdict(list)
     for r in rows:
@@ -97,7 +97,7 @@ def timed_dispatches(d):
         if len(per[k]) < lo + L:
             continue
         out[k] = per[k][lo:lo + L]
-    return out, events
+    return out, events, line
 
 
 def main():
@@ -140,7 +140,15 @@ def main():
                                           ("wait_inst_any", "SQ_WAIT_INST_ANY"),
                                           ("wait_any", "SQ_WAIT_ANY")) if c in sqm}
         res["kernels"][k] = e
-    timed, events = timed_dispatches(d)
+    timed, events, line = timed_dispatches(d)
+    if line is not None:  # the workload the profile was taken on (bench.py checks it against its own)
+        c = line.get("config", {})
+        res["profiled_workload"] = {"resolution": c.get("resolution"), "qp": c.get("qp"),
+                                    "sequence_frames": c.get("sequence_frames"),
+                                    "pairs_per_step_rank0": c.get("pairs_per_step_rank0"),
+                                    "modes": c.get("modes"), "rank_only": c.get("rank_only"),
+                                    "steps": line.get("steps"), "warmup": line.get("warmup"),
+                                    "native_sha256": (line.get("native") or {}).get("sha256")}
     for k, v in timed.items():
         e = res["kernels"].setdefault(k, {})
         e["timed_dispatches"] = len(v)

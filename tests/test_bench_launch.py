@@ -130,7 +130,8 @@ def test_bench_gpus2_launches_two_ranks(weak):
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["world"] == {"size": 2, "backend": "gloo", "launcher": "bench.py"}
+    assert d["n_gpus"] == 2 and d["world"] == {"size": 2, "backend": "gloo", "launcher": "bench.py",
+                                               "forced_pg": False}
     assert d["config"]["rows_per_step_all"] == 2 * d["config"]["rows_per_step_rank0"]
     assert d["gather"]["check"]["byte_identical"] is True
     assert d["step_ms"]["min"] <= d["step_ms"]["median"] <= d["step_ms"]["max"]
@@ -164,6 +165,7 @@ def test_bench_under_torchrun():
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["world"] == {"size": 2, "backend": "gloo", "launcher": "external"}
+    assert d["n_gpus"] == 2 and d["world"] == {"size": 2, "backend": "gloo", "launcher": "external",
+                                               "forced_pg": False}
     assert d["gather"]["check"]["byte_identical"] is True
     assert d["native"]["lib"].endswith("libvame.so")

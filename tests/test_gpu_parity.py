@@ -408,17 +408,19 @@ def test_property_translation_1080p(engines, d):
 
 
 @pytest.mark.parametrize("env", [{"VAME_HALF128": "0"}, {"VAME_STREAMS": "1"},
-                                 {"VAME_STREAMS": "1", "VAME_HALF128": "0"}],
-                         ids=["ctu1024_packing", "one_stream", "one_stream_ctu1024"])
+                                 {"VAME_STREAMS": "1", "VAME_HALF128": "0"}, {"VAME_GRAPH": "1"}],
+                         ids=["ctu1024_packing", "one_stream", "one_stream_ctu1024", "graph"])
 def test_launch_structure_variants(env, monkeypatch):
     """The engine's launch-structure knobs (read at vame_create) change only
     where the work runs: VAME_HALF128=0 puts the 128x64 / 64x128 CUs back into
     the 1024-thread CTU items (two CUs per workgroup) instead of one 512-thread
     affine_me_half workgroup each; VAME_STREAMS=1 issues every kernel of a call
     on the caller's stream (all but the first without the AQL barrier bit)
-    instead of forking a side stream.  A 1080p POC with 2 refs (2+3 CP) and a
-    2-CP-only POC give the default context's results bit for bit, and the
-    default equals the oracle on one pair."""
+    instead of forking a side stream; VAME_GRAPH=1 captures a call's launches
+    into a hipGraph and replays it when the call repeats (each call below runs
+    twice, the second from the graph, after its outputs were cleared).  A 1080p
+    POC with 2 refs (2+3 CP) and a 2-CP-only POC give the default context's
+    results bit for bit, and the default equals the oracle on one pair."""
     from vame.engine import Engine
     from vame import synth
     o, r = synth.synth_sequence(1920, 1080, 2, 32, seed=0x0DE6)
@@ -428,7 +430,16 @@ def test_launch_structure_variants(env, monkeypatch):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     eng = Engine(1920, 1080, 0)
-    got = {m: eng.affine_me_poc(cur, refs, 70.335619, modes=m) for m in (3, 1)}
+    got = {}
+    for m in (3, 1):
+        out = eng.alloc_poc(2, m)
+        eng.affine_me_poc(cur, refs, 70.335619, modes=m, out=out)
+        torch.cuda.synchronize()
+        for c, p in out.values():  # the repeat (a graph replay under VAME_GRAPH) must rewrite them
+            c.fill_(-1)
+            p.fill_(-1)
+        eng.affine_me_poc(cur, refs, 70.335619, modes=m, out=out)
+        got[m] = out
     torch.cuda.synchronize()
     for m in want:
         for k in want[m]:

@@ -57,6 +57,17 @@ struct vame_ctx {
   // VAME_STREAMS=1: every kernel of a call on the caller's stream, all but the
   // first without the AQL barrier bit (hipExtAnyOrderLaunch), no fork / join
   int streams = 2;
+  // VAME_GRAPH=1: a call's launch sequence (fork, kernels, join) is captured
+  // once into a hipGraph (on capStream) and replayed on the caller's stream
+  // whenever the same call -- the same kernel arguments -- repeats, e.g. the
+  // bench's steps; calls with kernel timing on launch directly
+  bool useGraph = false;
+  hipStream_t capStream = nullptr;
+  struct GraphEntry {
+    std::vector<unsigned char> key;
+    hipGraphExec_t exec;
+  };
+  std::vector<GraphEntry> graphs;  // most recent last, at most kMaxGraphs
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[3];
   size_t evUsed[3] = {0, 0, 0};
 };
@@ -358,8 +369,22 @@ KernelFn kernel_for(bool prof, int mode) {
   }
 }
 
-int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool quadHalf, bool bigItems,
-           hipStream_t stream) {
+constexpr size_t kMaxGraphs = 8;
+
+// Launch one kernel: with the dispatch-carried timing events and AQL flags, or
+// (stream capture) as a plain launch, which a graph records.
+template <typename K>
+hipError_t launch_kernel(K kernel, unsigned grid, unsigned threads, hipStream_t s, hipEvent_t t0, hipEvent_t t1,
+                         int flags, const KParams& kp, bool capture) {
+  if (capture)
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, kp);
+  else
+    hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, t0, t1, flags, kp);
+  return hipGetLastError();
+}
+
+int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool quadHalf, bool bigItems,
+                  hipStream_t stream, bool capture) {
   // 128-class items (big LDS, 1 workgroup per CU) and quadrant items run on
   // two streams so they overlap: the 128-class kernel on the caller's stream,
   // first, and the quadrant kernel on the side stream.  A 128-class
@@ -392,9 +417,8 @@ int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool qua
     const unsigned grid = block_grid(c, 1, kb);
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 1, t0, t1));
-    hipExtLaunchKernelGGL(kernel_for<kKindCtu>(c->prof, mode), dim3(grid), dim3(Cfg<kKindCtu>::THREADS), 0,
-                          sBig, t0, t1, order_flag(), kb);
-    VAME_HIP(hipGetLastError());
+    VAME_HIP(launch_kernel(kernel_for<kKindCtu>(c->prof, mode), grid, Cfg<kKindCtu>::THREADS, sBig, t0, t1,
+                           order_flag(), kb, capture));
     return VAME_OK;
   };
   auto half = [&](const KParams& kp) -> int {  // after the 128x128 items, on their stream
@@ -404,9 +428,8 @@ int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool qua
     const unsigned grid = block_grid(c, 1, kh);
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 2, t0, t1));
-    hipExtLaunchKernelGGL(kernel_for<kKindHalf>(c->prof, mode), dim3(grid), dim3(Cfg<kKindHalf>::THREADS), 0,
-                          sBig, t0, t1, order_flag(), kh);
-    VAME_HIP(hipGetLastError());
+    VAME_HIP(launch_kernel(kernel_for<kKindHalf>(c->prof, mode), grid, Cfg<kKindHalf>::THREADS, sBig, t0, t1,
+                           order_flag(), kh, capture));
     return VAME_OK;
   };
   auto quad = [&](const KParams& kp) -> int {
@@ -416,9 +439,8 @@ int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool qua
     const unsigned grid = block_grid(c, 0, kq);
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 0, t0, t1));
-    hipExtLaunchKernelGGL(kernel_for<kKindQuad>(c->prof, mode), dim3(grid), dim3(Cfg<kKindQuad>::THREADS), 0,
-                          sQuad, t0, t1, order_flag(), kq);
-    VAME_HIP(hipGetLastError());
+    VAME_HIP(launch_kernel(kernel_for<kKindQuad>(c->prof, mode), grid, Cfg<kKindQuad>::THREADS, sQuad, t0, t1,
+                           order_flag(), kq, capture));
     return VAME_OK;
   };
   auto all = [&]() -> int {
@@ -446,6 +468,50 @@ int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool qua
     if (hipEventRecord(c->evJoin, c->side) == hipSuccess) (void)hipStreamWaitEvent(stream, c->evJoin, 0);
   }
   return rc;
+}
+
+int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool quadHalf, bool bigItems,
+           hipStream_t stream) {
+  if (!c->useGraph || c->timing || kps.empty()) return launch_direct(c, kps, quadFull, quadHalf, bigItems, stream, false);
+  // the call's identity: its kernel arguments and launch selection
+  std::vector<unsigned char> key(kps.size() * sizeof(KParams) + 4);
+  for (size_t k = 0; k < kps.size(); k++) memcpy(key.data() + k * sizeof(KParams), &kps[k], sizeof(KParams));
+  unsigned char* tail = key.data() + kps.size() * sizeof(KParams);
+  tail[0] = quadFull;
+  tail[1] = quadHalf;
+  tail[2] = bigItems;
+  tail[3] = c->prof;
+  for (size_t i = 0; i < c->graphs.size(); i++) {
+    if (c->graphs[i].key == key) {
+      vame_ctx::GraphEntry e = std::move(c->graphs[i]);
+      c->graphs.erase(c->graphs.begin() + (long)i);
+      c->graphs.push_back(std::move(e));  // most recently used last
+      VAME_HIP(hipGraphLaunch(c->graphs.back().exec, stream));
+      return VAME_OK;
+    }
+  }
+  // capture on the engine's own stream (the caller's may be the null stream,
+  // which cannot be captured); the fork / join to the side stream become graph edges
+  VAME_HIP(hipStreamBeginCapture(c->capStream, hipStreamCaptureModeThreadLocal));
+  const int rc = launch_direct(c, kps, quadFull, quadHalf, bigItems, c->capStream, true);
+  hipGraph_t g = nullptr;
+  const hipError_t ec = hipStreamEndCapture(c->capStream, &g);
+  if (rc != VAME_OK || ec != hipSuccess) {
+    if (g) (void)hipGraphDestroy(g);
+    if (rc != VAME_OK) return rc;
+    VAME_HIP(ec);
+  }
+  hipGraphExec_t exec = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  VAME_HIP(ei);
+  if (c->graphs.size() == kMaxGraphs) {
+    (void)hipGraphExecDestroy(c->graphs.front().exec);
+    c->graphs.erase(c->graphs.begin());
+  }
+  c->graphs.push_back({std::move(key), exec});
+  VAME_HIP(hipGraphLaunch(exec, stream));
+  return VAME_OK;
 }
 
 }  // namespace
@@ -514,6 +580,7 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   const int xcdOrder = env_int("VAME_XCD_ORDER", 0);
   c->joinEach = env_int("VAME_JOIN_EACH", 0) != 0;
   c->streams = env_int("VAME_STREAMS", 2) == 1 ? 1 : 2;
+  c->useGraph = env_int("VAME_GRAPH", 0) != 0;
   c->groupCombos[0] = std::max(8, env_int("VAME_GROUP_COMBOS", 408));
   c->groupCombos[1] = std::max(8, env_int("VAME_GROUP_COMBOS_BIG", c->groupCombos[0]));
   for (int k = 0; k < 2 && e == hipSuccess; k++) {
@@ -532,6 +599,7 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming);
+  if (e == hipSuccess && c->useGraph) e = hipStreamCreateWithFlags(&c->capStream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     snprintf(g_hip_err, sizeof(g_hip_err), "%s", hipGetErrorString(e));
     vame_destroy(c);
@@ -549,6 +617,8 @@ void vame_destroy(vame_ctx* c) {
   if (c->dHalf) (void)hipFree(c->dHalf);
   for (int k = 0; k < 2; k++)
     if (c->dOrder[k]) (void)hipFree(c->dOrder[k]);
+  for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
+  if (c->capStream) (void)hipStreamDestroy(c->capStream);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->evFork) (void)hipEventDestroy(c->evFork);
   if (c->evJoin) (void)hipEventDestroy(c->evJoin);

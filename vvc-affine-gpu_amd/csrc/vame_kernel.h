@@ -1468,6 +1468,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   constexpr bool run2 = (MODE & 1) != 0, run3 = (MODE & 2) != 0;
   using C = Cfg<KIND>;
   constexpr int REGION = C::REGION;  // instrumentation slots: 128 = the 128-class kernels
+  (void)REGION;
   __shared__ __attribute__((aligned(16))) uint16_t s_tile[C::TILE_ELEMS];
   static_assert((C::TP * 2) % 16 == 0 && C::TILE % 8 == 0, "16-byte tile rows");
   __shared__ uint2 s_top[C::NSB];  // row 0 of every sub-block's prediction (packed pairs)
