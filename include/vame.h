@@ -116,6 +116,15 @@ int vame_set_prof(vame_ctx* ctx, int enable);
 int vame_set_timing(vame_ctx* ctx, int enable);
 int vame_get_timing(vame_ctx* ctx, int kernel_class, double* total_ms, int* launches, int reset);
 
+/* Work-item templates (no device work): how many times the engine's work
+ * items -- quadrant, 128x128 and 128x64 / 64x128 items, as vame_create builds
+ * them with half128 = the VAME_HALF128 setting -- cover each of the CTU's
+ * candidate CUs of `align`: hits[0 .. {201|284}) indexed by the output offset
+ * RETURN_STRIDE[group] + cuIdx (affine.cl:936 / :1929).  A valid partition
+ * covers every CU exactly once.  Also returns the item counts per kernel
+ * class (quad, ctu, half) in items3 when non-NULL. */
+int vame_template_coverage(int half128, int align, int32_t* hits, int32_t* items3);
+
 /* Geometry / host helpers (no device work). */
 int vame_num_ctus(int width, int height);   /* 0 if unsupported */
 int vame_cus_per_ctu(int align);            /* 201 / 284 */

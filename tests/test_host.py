@@ -47,6 +47,24 @@ def test_version_and_errors():
     assert L.vame_cus_per_ctu(0) == 201 and L.vame_cus_per_ctu(1) == 284
 
 
+@pytest.mark.parametrize("half128", [1, 0])
+def test_work_items_cover_every_cu_once(half128):
+    """The engine's work-item templates (vame_create's build_templates, run on
+    the host without a device) partition the CTU's candidate CUs: every FULL
+    (201) and HALF (284) output offset is covered by exactly one item's CU
+    slot -- with the 128x64 / 64x128 CUs in 512-thread affine_me_half items
+    (one CU each, the default) or packed two per 1024-thread CTU item."""
+    L = _lib.lib()
+    items = (ctypes.c_int32 * 3)()
+    for align, n in ((0, 201), (1, 284)):
+        hits = (ctypes.c_int32 * n)()
+        assert L.vame_template_coverage(half128, align, hits, items) == 0
+        assert list(hits) == [1] * n, (align, [i for i in range(n) if hits[i] != 1])
+    quad, ctu, half = list(items)
+    assert quad > 0
+    assert (ctu, half) == ((1, 4) if half128 else (3, 0))
+
+
 @pytest.mark.parametrize("row", GOLD["lambda"], ids=lambda r: f"qp{r['qp']}_poc{r['poc']}")
 def test_lambda_and_qp(row):
     assert poc_qp(row["qp"], row["poc"]) == row["poc_qp"]

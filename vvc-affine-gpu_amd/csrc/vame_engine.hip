@@ -655,6 +655,28 @@ int vame_affine_me(vame_ctx* c, const uint16_t* ref, const uint16_t* cur, float 
   return launch(c, std::vector<KParams>{kp}, align == 0, align == 1, align == 0, (hipStream_t)stream);
 }
 
+int vame_template_coverage(int half128, int align, int32_t* hits, int32_t* items3) {
+  if (!hits || (align != 0 && align != 1)) return VAME_E_INVALID;
+  std::vector<Item> big, hf, qf, qh;
+  build_templates(big, hf, qf, qh, half128 != 0);
+  const int n = align ? kHalfCusPerCtu : kFullCusPerCtu;
+  for (int i = 0; i < n; i++) hits[i] = 0;
+  for (const auto* v : {&big, &hf, &qf, &qh})
+    for (const Item& it : *v)
+      for (int k = 0; k < it.nCu; k++) {
+        const CuSlot& s = it.cu[k];
+        if (s.align != align) continue;
+        if (s.outOff < 0 || s.outOff >= n) return VAME_E_INVALID;
+        hits[s.outOff]++;
+      }
+  if (items3) {
+    items3[0] = (int32_t)(qf.size() + qh.size());
+    items3[1] = (int32_t)big.size();
+    items3[2] = (int32_t)hf.size();
+  }
+  return VAME_OK;
+}
+
 int vame_pred_mask(int mode_mask) {
   const int ncp = (mode_mask & VAME_MODE_3CP) ? 3 : 1;  // 2CP [+ 3CP] per alignment
   const int sel = (mode_mask >> 2) & 3;                  // neither selection bit: both

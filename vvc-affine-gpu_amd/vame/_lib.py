@@ -18,7 +18,7 @@ EXPORTS = (
     "vame_log_writer_create", "vame_log_writer_poc", "vame_log_writer_destroy", "vame_pred_mask",
     "vame_log_writer_refs", "vame_read_frames_range", "vame_count_lines", "vame_read_frames_span",
     "vame_log_writer_set_deferred", "vame_log_writer_num_files", "vame_log_writer_file_name",
-    "vame_log_writer_sizes", "vame_log_writer_flush_at",
+    "vame_log_writer_sizes", "vame_log_writer_flush_at", "vame_template_coverage",
 )
 
 
