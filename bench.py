@@ -232,13 +232,17 @@ def main():
     quad_bytes = acc["bytes_quad"] * run.pairs * args.steps
     achieved = quad_bytes / (quad_ms * 1e-3) / 1e9 if quad_ms > 0 else 0.0
     # per 128-class kernel: its dispatches' average and the algorithmic bytes
-    # it carries (VAME_HALF128=0: every 128-class CU in affine_me_ctu)
+    # it carries: with affine_me_half launches (a launch of >= 16 pairs, the
+    # engine's default) the CTU items hold only the 128x128 CUs; otherwise all
+    # 128-class CUs (a mix of both packings in one step leaves the CTU kernel's
+    # bytes unattributed)
     split = big_t[2][1] > 0
+    mixed = split and big_t[2][1] != big_t[1][1]
     big_kernels = {}
     for k, name, key in ((1, "affine_me_ctu", "bytes_ctu" if split else "bytes_big"),
                          (2, "affine_me_half", "bytes_half")):
         ms, n = big_t[k]
-        if n == 0:
+        if n == 0 or (mixed and k == 1):
             continue
         b = acc[key] * run.pairs * big_steps
         ach = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0

@@ -108,8 +108,9 @@ int vame_set_prof(vame_ctx* ctx, int enable);
 /* Device-side kernel timing (the reference's per-PRED kernelExecutionTime,
  * main.cpp:856-866): when enabled, every kernel launch carries hipEvents in its
  * own dispatch on the stream it runs on.  kernel_class 0 = quadrant work items
- * (affine_me_quad), 1 = 128x128 CUs (affine_me_ctu), 2 = 128x64 / 64x128 CUs
- * (affine_me_half; with VAME_HALF128=0 at vame_create they run in class 1).
+ * (affine_me_quad), 1 = CTU items (affine_me_ctu: the 128x128 CUs, and in
+ * launches of fewer than VAME_HALF_MIN_PAIRS pairs -- or with VAME_HALF128=0 --
+ * the 128x64 / 64x128 CUs too), 2 = single 128x64 / 64x128 CUs (affine_me_half).
  * enable = 2 times the quadrant kernel only (its dispatches carry the events;
  * the 128-class launches run untimed).  vame_get_timing waits for the recorded
  * launches and returns their summed duration and count since the last reset. */
@@ -118,7 +119,7 @@ int vame_get_timing(vame_ctx* ctx, int kernel_class, double* total_ms, int* laun
 
 /* Work-item templates (no device work): how many times the engine's work
  * items -- quadrant, 128x128 and 128x64 / 64x128 items, as vame_create builds
- * them with half128 = the VAME_HALF128 setting -- cover each of the CTU's
+ * them; half128 != 0: the affine_me_half packing, 0: the CTU packing -- cover each of the CTU's
  * candidate CUs of `align`: hits[0 .. {201|284}) indexed by the output offset
  * RETURN_STRIDE[group] + cuIdx (affine.cl:936 / :1929).  A valid partition
  * covers every CU exactly once.  Also returns the item counts per kernel

@@ -231,6 +231,24 @@ def test_live_reference_configs(engines, tmp_path, W, H, qp, poc, refidx):
     job = (dev(orig[poc]), d_refs, lam, eng.alloc_poc(len(refs), 3))
     eng.affine_me_batch([job], 3, 0)
     check_vs_live_reference(runs, job[3], lambda name: (refidx, name), recon[rp], orig[poc], lam)
+    # both packings of the 128-class CUs: this short launch ran the CTU items;
+    # the long launches of the configs run affine_me_half (VAME_HALF128=1 here)
+    from vame.engine import Engine
+    old = os.environ.get("VAME_HALF128")
+    os.environ["VAME_HALF128"] = "1"
+    try:
+        eng_half = Engine(W, H, 0)
+    finally:
+        if old is None:
+            del os.environ["VAME_HALF128"]
+        else:
+            os.environ["VAME_HALF128"] = old
+    try:
+        job_h = (job[0], d_refs, lam, eng_half.alloc_poc(len(refs), 3))
+        eng_half.affine_me_batch([job_h], 3, 0)
+        check_vs_live_reference(runs, job_h[3], lambda name: (refidx, name), recon[rp], orig[poc], lam)
+    finally:
+        eng_half.close()
 
 
 PROF_CASES = [p for p in GOLDEN if any(k in p for k in ("qp32_poc1", "bigmotion", "extra1", "s832"))]
@@ -407,14 +425,17 @@ def test_property_translation_1080p(engines, d):
     assert n > 1000 and frac >= 0.75, (frac, n)
 
 
-@pytest.mark.parametrize("env", [{"VAME_HALF128": "0"}, {"VAME_STREAMS": "1"},
-                                 {"VAME_STREAMS": "1", "VAME_HALF128": "0"}, {"VAME_GRAPH": "1"}],
-                         ids=["ctu1024_packing", "one_stream", "one_stream_ctu1024", "graph"])
+@pytest.mark.parametrize("env", [{"VAME_HALF128": "1"}, {"VAME_HALF128": "0"}, {"VAME_STREAMS": "1"},
+                                 {"VAME_STREAMS": "1", "VAME_HALF128": "1"}, {"VAME_GRAPH": "1"},
+                                 {"VAME_GRAPH": "1", "VAME_HALF128": "1"}],
+                         ids=["half512_packing", "ctu1024_packing", "one_stream", "one_stream_half512", "graph",
+                              "graph_half512"])
 def test_launch_structure_variants(env, monkeypatch):
     """The engine's launch-structure knobs (read at vame_create) change only
-    where the work runs: VAME_HALF128=0 puts the 128x64 / 64x128 CUs back into
-    the 1024-thread CTU items (two CUs per workgroup) instead of one 512-thread
-    affine_me_half workgroup each; VAME_STREAMS=1 issues every kernel of a call
+    where the work runs: VAME_HALF128=1 gives every 128x64 / 64x128 CU a
+    512-thread affine_me_half workgroup of its own, 0 keeps them in the
+    1024-thread CTU items (two CUs per workgroup; the default for launches of
+    fewer than 16 pairs, as here); VAME_STREAMS=1 issues every kernel of a call
     on the caller's stream (all but the first without the AQL barrier bit)
     instead of forking a side stream; VAME_GRAPH=1 captures a call's launches
     into a hipGraph and replays it when the call repeats (each call below runs

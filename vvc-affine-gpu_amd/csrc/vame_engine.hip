@@ -36,11 +36,23 @@ static thread_local char g_hip_err[256] = "";
 
 struct vame_ctx {
   int device, W, H, nCtus, ctusPerRow;
-  // device-resident work-item templates: [quadFull | quadHalf] and big (FULL 128-class)
+  // device-resident work-item templates: [quadFull | quadHalf] and the FULL
+  // 128-class CUs in two packings: dBig3 -- the 128x128, 128x64 and 64x128
+  // groups as 1024-thread CTU items (affine_me_ctu); or dBig1 (the 128x128
+  // item) + dHalf (each 128x64 / 64x128 CU alone, affine_me_half)
   Item* dQuad = nullptr;
-  Item* dBig = nullptr;
-  Item* dHalf = nullptr;  // affine_me_half items: one 128x64 / 64x128 CU each (VAME_HALF128, default on)
-  int nQuadFull = 0, nQuadHalf = 0, nBig = 0, nHalf = 0;
+  Item* dBig3 = nullptr;
+  Item* dBig1 = nullptr;
+  Item* dHalf = nullptr;
+  int nQuadFull = 0, nQuadHalf = 0, nBig3 = 0, nBig1 = 0, nHalf = 0;
+  // which packing a launch uses (VAME_HALF128): 0 always dBig3, 1 always
+  // dBig1 + dHalf, 2 (default) dBig1 + dHalf for launches of at least
+  // halfMinPairs (POC, refIdx) pairs (VAME_HALF_MIN_PAIRS, default 16), dBig3
+  // below: a short launch (the 3-pair c2 step) ends sooner with the 128-class
+  // work in the early-starting CTU items, a long one (32 pairs) gains from the
+  // smaller workgroups sharing CUs
+  int halfMode = 2, halfMinPairs = 16;
+  bool quadFirst = false;  // VAME_QUAD_FIRST=1 (with VAME_STREAMS=1): the quadrant kernel issued first
   // block order (block_grid), per kernel class (0 quadrant, 1 128-class):
   // slot -> CTU table, group size, CTU chunks, slots per (pair, chunk)
   int32_t* dOrder[2] = {nullptr, nullptr};
@@ -410,10 +422,13 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
     VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
     sQuad = c->side;
   }
+  auto use_half = [&](const KParams& kp) {
+    return c->halfMode == 1 || (c->halfMode == 2 && kp.nPairs >= c->halfMinPairs);
+  };
   auto big = [&](const KParams& kp) -> int {
     KParams kb = kp;
-    kb.items = c->dBig;
-    kb.nItems = c->nBig;
+    kb.items = use_half(kp) ? c->dBig1 : c->dBig3;
+    kb.nItems = use_half(kp) ? c->nBig1 : c->nBig3;
     const unsigned grid = block_grid(c, 1, kb);
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 1, t0, t1));
@@ -445,9 +460,11 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
   };
   auto all = [&]() -> int {
     for (size_t k = 0; k < kps.size(); k++) {
-      if (bigItems && c->nBig) VAME_TRY(big(kps[k]));
-      if (bigItems && c->nHalf) VAME_TRY(half(kps[k]));
-      if (quadFull || quadHalf) VAME_TRY(quad(kps[k]));
+      const bool quadFirst = c->streams == 1 && c->quadFirst;  // VAME_QUAD_FIRST (one-stream mode)
+      if (quadFirst && (quadFull || quadHalf)) VAME_TRY(quad(kps[k]));
+      if (bigItems) VAME_TRY(big(kps[k]));
+      if (bigItems && use_half(kps[k])) VAME_TRY(half(kps[k]));
+      if (!quadFirst && (quadFull || quadHalf)) VAME_TRY(quad(kps[k]));
       if (fork && (c->joinEach || k + 1 == kps.size())) {
         VAME_HIP(hipEventRecord(c->evJoin, c->side));
         VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
@@ -561,16 +578,22 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (device < 0 || device >= ndev) return VAME_E_INVALID;
   DeviceGuard guard(device);
   VAME_HIP(guard.err);
-  std::vector<Item> big, hf, qf, qh;
-  build_templates(big, hf, qf, qh, env_int("VAME_HALF128", 1) != 0);
+  std::vector<Item> big3, big1, hf, qf, qh, unused;
+  build_templates(big3, unused, qf, qh, false);
+  qf.clear();
+  qh.clear();
+  build_templates(big1, hf, qf, qh, true);
   vame_ctx* c = new vame_ctx();
   c->device = device;
   c->W = width;
   c->H = height;
   c->nCtus = nCtus;
   c->ctusPerRow = (width + kCtu - 1) / kCtu;  // T8: integer ceil
-  c->nBig = (int)big.size();
+  c->nBig3 = (int)big3.size();
+  c->nBig1 = (int)big1.size();
   c->nHalf = (int)hf.size();
+  c->halfMode = std::min(2, std::max(0, env_int("VAME_HALF128", 2)));
+  c->halfMinPairs = std::max(1, env_int("VAME_HALF_MIN_PAIRS", 16));
   c->nQuadFull = (int)qf.size();
   c->nQuadHalf = (int)qh.size();
   std::vector<Item> quad(qf);
@@ -581,6 +604,7 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   c->joinEach = env_int("VAME_JOIN_EACH", 0) != 0;
   c->streams = env_int("VAME_STREAMS", 2) == 1 ? 1 : 2;
   c->useGraph = env_int("VAME_GRAPH", 0) != 0;
+  c->quadFirst = env_int("VAME_QUAD_FIRST", 0) != 0;
   c->groupCombos[0] = std::max(8, env_int("VAME_GROUP_COMBOS", 408));
   c->groupCombos[1] = std::max(8, env_int("VAME_GROUP_COMBOS_BIG", c->groupCombos[0]));
   for (int k = 0; k < 2 && e == hipSuccess; k++) {
@@ -590,9 +614,11 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
     if (e == hipSuccess)
       e = hipMemcpy(c->dOrder[k], order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice);
   }
-  if (e == hipSuccess) e = hipMalloc(&c->dBig, big.size() * sizeof(Item));
+  if (e == hipSuccess) e = hipMalloc(&c->dBig3, big3.size() * sizeof(Item));
+  if (e == hipSuccess) e = hipMalloc(&c->dBig1, big1.size() * sizeof(Item));
   if (e == hipSuccess) e = hipMemcpy(c->dQuad, quad.data(), quad.size() * sizeof(Item), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(c->dBig, big.data(), big.size() * sizeof(Item), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->dBig3, big3.data(), big3.size() * sizeof(Item), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->dBig1, big1.data(), big1.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess && !hf.empty()) e = hipMalloc(&c->dHalf, hf.size() * sizeof(Item));
   if (e == hipSuccess && !hf.empty())
     e = hipMemcpy(c->dHalf, hf.data(), hf.size() * sizeof(Item), hipMemcpyHostToDevice);
@@ -613,7 +639,8 @@ void vame_destroy(vame_ctx* c) {
   if (!c) return;
   DeviceGuard guard(c->device);
   if (c->dQuad) (void)hipFree(c->dQuad);
-  if (c->dBig) (void)hipFree(c->dBig);
+  if (c->dBig3) (void)hipFree(c->dBig3);
+  if (c->dBig1) (void)hipFree(c->dBig1);
   if (c->dHalf) (void)hipFree(c->dHalf);
   for (int k = 0; k < 2; k++)
     if (c->dOrder[k]) (void)hipFree(c->dOrder[k]);
