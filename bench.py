@@ -167,12 +167,19 @@ def main():
     # its dispatches too cost ~0.7 % of a c2 step).  Diagnostic override
     # VAME_BENCH_KTIMING: 0 = no events, 1 = both kernels in the timed steps.
     ktiming = int(os.environ.get("VAME_BENCH_KTIMING", "2"))
+    # the events ride on a sample of the timed steps -- every ksample-th step
+    # (VAME_BENCH_KSAMPLE, default 4) -- so the timed span carries a quarter of
+    # their cost (in the engine's one-stream mode a dispatch with events costs
+    # ~0.7 % of a c2 step)
+    ksample = max(1, int(os.environ.get("VAME_BENCH_KSAMPLE", "4")))
     eng.set_timing(ktiming)
     # one event per step boundary on the issuing stream: the per-step spread
     step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t_start = time.perf_counter()
     step_ev[0].record()
     for i in range(args.steps):
+        if ksample > 1:
+            eng.set_timing(ktiming if i % ksample == 0 else 0, keep=True)
         run.step()
         step_ev[i + 1].record()
     barrier()
@@ -303,6 +310,10 @@ def main():
                      "kernel": "affine_me_quad",
                      "avg_launch_ms": quad_ms / max(quad_n, 1),
                      "launches": quad_n,
+                     # the timed steps whose quadrant dispatches carry the events
+                     "timed_sample": {"every": ksample,
+                                      "steps": len(range(0, args.steps, ksample)) if ktiming else 0,
+                                      "launches_per_step": -(-run.pairs // 32)},
                      # the same kernel's average under rocprofv3 over the timed
                      # dispatches of a traced run of this config (profiles/)
                      "rocprof_avg_ms": prof.get("rocprof_avg_ms"),

@@ -113,7 +113,10 @@ int vame_set_prof(vame_ctx* ctx, int enable);
  * the 128x64 / 64x128 CUs too), 2 = single 128x64 / 64x128 CUs (affine_me_half).
  * enable = 2 times the quadrant kernel only (its dispatches carry the events;
  * the 128-class launches run untimed).  vame_get_timing waits for the recorded
- * launches and returns their summed duration and count since the last reset. */
+ * launches and returns their summed duration and count since the last reset.
+ * enable | VAME_TIMING_KEEP changes what later launches record without
+ * dropping the launches recorded so far (timing a sample of a run's steps). */
+enum { VAME_TIMING_KEEP = 16 };
 int vame_set_timing(vame_ctx* ctx, int enable);
 int vame_get_timing(vame_ctx* ctx, int kernel_class, double* total_ms, int* launches, int reset);
 

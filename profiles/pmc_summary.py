@@ -84,6 +84,8 @@ def timed_dispatches(d):
     K, W = line["steps"], line["warmup"]
     P = (line.get("prewarm") or {}).get("steps", 0)
     roof = line["roofline"]
+    ts = roof.get("timed_sample") or {}
+    lps = ts.get("launches_per_step")  # the quadrant kernel's launches per step (sampled events)
     launches = {"affine_me_quad": roof.get("launches")}
     events = {"affine_me_quad": roof.get("avg_launch_ms")}
     for k in ("affine_me_ctu", "affine_me_half"):  # the 128-class kernels (timed on their own steps)
@@ -91,6 +93,8 @@ def timed_dispatches(d):
         events[k] = roof.get(k, {}).get("avg_launch_ms")
     out = {}
     for k, L in launches.items():
+        if k == "affine_me_quad" and lps:  # every timed dispatch, sampled events or not
+            L = lps * K
         if not L or L % K or k not in per:
             continue
         lo = (P + W) * (L // K)

@@ -425,19 +425,21 @@ def test_property_translation_1080p(engines, d):
     assert n > 1000 and frac >= 0.75, (frac, n)
 
 
-@pytest.mark.parametrize("env", [{"VAME_HALF128": "1"}, {"VAME_HALF128": "0"}, {"VAME_STREAMS": "1"},
-                                 {"VAME_STREAMS": "1", "VAME_HALF128": "1"}, {"VAME_GRAPH": "1"},
-                                 {"VAME_GRAPH": "1", "VAME_HALF128": "1"}],
-                         ids=["half512_packing", "ctu1024_packing", "one_stream", "one_stream_half512", "graph",
-                              "graph_half512"])
+@pytest.mark.parametrize("env", [{"VAME_HALF128": "1"}, {"VAME_HALF128": "0"}, {"VAME_STREAMS": "2"},
+                                 {"VAME_STREAMS": "2", "VAME_HALF128": "1"}, {"VAME_QUAD_FIRST": "0"},
+                                 {"VAME_GRAPH": "1"}, {"VAME_GRAPH": "1", "VAME_HALF128": "1"},
+                                 {"VAME_GRAPH": "1", "VAME_STREAMS": "2"}],
+                         ids=["half512_packing", "ctu1024_packing", "two_streams", "two_streams_half512",
+                              "ctu_first", "graph", "graph_half512", "graph_two_streams"])
 def test_launch_structure_variants(env, monkeypatch):
     """The engine's launch-structure knobs (read at vame_create) change only
     where the work runs: VAME_HALF128=1 gives every 128x64 / 64x128 CU a
     512-thread affine_me_half workgroup of its own, 0 keeps them in the
     1024-thread CTU items (two CUs per workgroup; the default for launches of
-    fewer than 16 pairs, as here); VAME_STREAMS=1 issues every kernel of a call
-    on the caller's stream (all but the first without the AQL barrier bit)
-    instead of forking a side stream; VAME_GRAPH=1 captures a call's launches
+    fewer than 16 pairs, as here); VAME_STREAMS=2 forks a side stream for the
+    quadrant kernel instead of issuing every kernel of a call on the caller's
+    stream (all but the first without the AQL barrier bit, the default);
+    VAME_QUAD_FIRST=0 issues the 128-class kernels before the quadrant kernel; VAME_GRAPH=1 captures a call's launches
     into a hipGraph and replays it when the call repeats (each call below runs
     twice, the second from the graph, after its outputs were cleared).  A 1080p
     POC with 2 refs (2+3 CP) and a 2-CP-only POC give the default context's

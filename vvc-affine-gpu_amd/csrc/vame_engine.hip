@@ -52,7 +52,10 @@ struct vame_ctx {
   // work in the early-starting CTU items, a long one (32 pairs) gains from the
   // smaller workgroups sharing CUs
   int halfMode = 2, halfMinPairs = 16;
-  bool quadFirst = false;  // VAME_QUAD_FIRST=1 (with VAME_STREAMS=1): the quadrant kernel issued first
+  // VAME_QUAD_FIRST (one-stream mode, default 1): the quadrant kernel issued
+  // first (it carries the call's barrier bit, the 128-class kernels follow it
+  // in any order)
+  bool quadFirst = true;
   // block order (block_grid), per kernel class (0 quadrant, 1 128-class):
   // slot -> CTU table, group size, CTU chunks, slots per (pair, chunk)
   int32_t* dOrder[2] = {nullptr, nullptr};
@@ -66,9 +69,13 @@ struct vame_ctx {
   bool prof = false;
   // VAME_JOIN_EACH=1: join the two streams after every launch of a batch
   bool joinEach = false;
-  // VAME_STREAMS=1: every kernel of a call on the caller's stream, all but the
-  // first without the AQL barrier bit (hipExtAnyOrderLaunch), no fork / join
-  int streams = 2;
+  // Streams of a call (VAME_STREAMS): 1 (default) -- every kernel on the
+  // caller's stream, all but the call's first without the AQL barrier bit
+  // (hipExtAnyOrderLaunch), so they overlap with no fork / join between
+  // streams (a c2 step boundary idles ~6 us instead of ~18); 2 -- the
+  // 128-class kernels on the caller's stream, the quadrant kernel on a side
+  // stream forked from it and joined at the end of the call
+  int streams = 1;
   // VAME_GRAPH=1: a call's launch sequence (fork, kernels, join) is captured
   // once into a hipGraph (on capStream) and replayed on the caller's stream
   // whenever the same call -- the same kernel arguments -- repeats, e.g. the
@@ -602,9 +609,9 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   // tuning knobs of the block order (defaults measured on MI355X)
   const int xcdOrder = env_int("VAME_XCD_ORDER", 0);
   c->joinEach = env_int("VAME_JOIN_EACH", 0) != 0;
-  c->streams = env_int("VAME_STREAMS", 2) == 1 ? 1 : 2;
+  c->streams = env_int("VAME_STREAMS", 1) == 2 ? 2 : 1;
   c->useGraph = env_int("VAME_GRAPH", 0) != 0;
-  c->quadFirst = env_int("VAME_QUAD_FIRST", 0) != 0;
+  c->quadFirst = env_int("VAME_QUAD_FIRST", 1) != 0;
   c->groupCombos[0] = std::max(8, env_int("VAME_GROUP_COMBOS", 408));
   c->groupCombos[1] = std::max(8, env_int("VAME_GROUP_COMBOS_BIG", c->groupCombos[0]));
   for (int k = 0; k < 2 && e == hipSuccess; k++) {
@@ -776,9 +783,13 @@ int vame_set_prof(vame_ctx* c, int enable) {
 
 int vame_set_timing(vame_ctx* c, int enable) {
   if (!c) return VAME_E_INVALID;
-  // kernel classes timed: bit 0 quadrant, bit 1 128x128, bit 2 128x64 / 64x128
+  // kernel classes timed: bit 0 quadrant, bit 1 CTU items, bit 2 half items;
+  // VAME_TIMING_KEEP (16) keeps the launches recorded so far (a caller timing
+  // a sample of its steps toggles timing between them)
+  const bool keep = (enable & VAME_TIMING_KEEP) != 0;
+  enable &= ~VAME_TIMING_KEEP;
   c->timing = enable == 2 ? 1 : enable != 0 ? 7 : 0;
-  c->evUsed[0] = c->evUsed[1] = c->evUsed[2] = 0;
+  if (!keep) c->evUsed[0] = c->evUsed[1] = c->evUsed[2] = 0;
   return VAME_OK;
 }
 

@@ -65,9 +65,10 @@ class Engine:
         affine.cl:168); vame_set_prof."""
         check(lib().vame_set_prof(self._h, int(enable)))
 
-    def set_timing(self, enable) -> None:
-        """True / 1: time every kernel class; 2: the quadrant kernel only; 0: off."""
-        check(lib().vame_set_timing(self._h, int(enable)))
+    def set_timing(self, enable, keep: bool = False) -> None:
+        """True / 1: time every kernel class; 2: the quadrant kernel only; 0: off.
+        keep: leave the launches recorded so far (VAME_TIMING_KEEP)."""
+        check(lib().vame_set_timing(self._h, int(enable) | (16 if keep else 0)))
 
     def get_timing(self, kernel_class: int, reset: bool = True):
         """(total_ms, launches) of kernel class 0 (quadrant items, affine_me_quad) /
