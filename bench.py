@@ -236,7 +236,10 @@ def main():
     del slabs
 
     # roofline of the dominant kernel (quadrant work items, affine_me_quad)
-    quad_bytes = acc["bytes_quad"] * run.pairs * args.steps
+    # the algorithmic bytes of the timed steps whose quadrant dispatches carried
+    # events (every ksample-th; each step is `launches_per_step` launches)
+    launches_per_step = -(-run.pairs // 32)
+    quad_bytes = acc["bytes_quad"] * run.pairs * (quad_n / launches_per_step)
     achieved = quad_bytes / (quad_ms * 1e-3) / 1e9 if quad_ms > 0 else 0.0
     # per 128-class kernel: its dispatches' average and the algorithmic bytes
     # it carries: with affine_me_half launches (a launch of >= 16 pairs, the
@@ -313,7 +316,7 @@ def main():
                      # the timed steps whose quadrant dispatches carry the events
                      "timed_sample": {"every": ksample,
                                       "steps": len(range(0, args.steps, ksample)) if ktiming else 0,
-                                      "launches_per_step": -(-run.pairs // 32)},
+                                      "launches_per_step": launches_per_step},
                      # the same kernel's average under rocprofv3 over the timed
                      # dispatches of a traced run of this config (profiles/)
                      "rocprof_avg_ms": prof.get("rocprof_avg_ms"),
