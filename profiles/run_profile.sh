@@ -37,4 +37,7 @@ if [ -f $R/vvc-affine-gpu_amd/lib/libvame_count.so ]; then
   cat $O/count.json
 fi
 python3 $R/profiles/pmc_summary.py $O $O/summary.json > /dev/null
+if [ -n "${CLEAN:-}" ]; then  # big configs: keep the summary, stats and logs (gpurun returns <= 64 MiB)
+  rm -f $O/trace/run_kernel_trace.csv $O/pmc_*/run_counter_collection.csv
+fi
 echo profile-done
