@@ -173,18 +173,26 @@ def main():
     # ~0.7 % of a c2 step)
     ksample = max(1, int(os.environ.get("VAME_BENCH_KSAMPLE", "4")))
     eng.set_timing(ktiming)
-    # one event per step boundary on the issuing stream: the per-step spread
-    step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    # the per-step spread: HIP events around the sampled steps only (an event
+    # record is a marker packet between two steps' kernels); VAME_BENCH_STEPEV=all
+    # brackets every step
+    every_step = os.environ.get("VAME_BENCH_STEPEV", "sampled") == "all"
+    step_ev = []
     t_start = time.perf_counter()
-    step_ev[0].record()
     for i in range(args.steps):
+        sampled = i % ksample == 0
         if ksample > 1:
-            eng.set_timing(ktiming if i % ksample == 0 else 0, keep=True)
+            eng.set_timing(ktiming if sampled else 0, keep=True)
+        if every_step or sampled:
+            a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a_.record()
         run.step()
-        step_ev[i + 1].record()
+        if every_step or sampled:
+            b_.record()
+            step_ev.append((a_, b_))
     barrier()
     elapsed = time.perf_counter() - t_start
-    step_ms = sorted(step_ev[i].elapsed_time(step_ev[i + 1]) for i in range(args.steps))
+    step_ms = sorted(a_.elapsed_time(b_) for a_, b_ in step_ev)
     quad_ms, quad_n = eng.get_timing(0)
     # the 128-class kernels (128x128 CUs: affine_me_ctu, class 1; 128x64 /
     # 64x128 CUs: affine_me_half, class 2), timed in the timed steps only with
@@ -275,8 +283,9 @@ def main():
         "warmup": args.warmup,
         "prewarm": {"seconds": args.prewarm_s, "steps": prewarm_steps},
         "ms_per_step": tmax * 1e3 / args.steps,
-        # rank 0's per-step GPU times (HIP events at the step boundaries)
-        "step_ms": {"median": step_ms[len(step_ms) // 2], "min": step_ms[0], "max": step_ms[-1]},
+        # rank 0's per-step GPU times (HIP events around the sampled steps)
+        "step_ms": {"median": step_ms[len(step_ms) // 2], "min": step_ms[0], "max": step_ms[-1],
+                    "steps": len(step_ms)},
         "world": {"size": world, "backend": "none" if dist is None else dist.get_backend(),
                   "launcher": os.environ.get("VAME_LAUNCHER", "external" if world > 1 else "none"),
                   # VAME_FORCE_PG=1: a one-rank process group, so the N-GPU
