@@ -31,43 +31,44 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     args = ap.parse_args()
     from bench import CONFIGS
-    from vame import synth, _lib
+    from vame import _lib
     from vame.engine import Engine
-    from vame.hostlogic import lambda_for_poc, ref_list
+    from vame.seqrun import ShardRun
+    from vame.shard import frames_for_pairs, sequence_pairs
     cfg = CONFIGS[args.config]
     W, H, qp, nf, modes = cfg["W"], cfg["H"], cfg["qp"], cfg["frames"], cfg["modes"]
     L = _lib.lib()
     fn = L.vame_debug_phase_cycles
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
     dev = torch.device("cuda", 0)
-    orig, recon = synth.synth_sequence(W, H, nf, qp, seed=0x5EED)
-    d_o = [torch.from_numpy(orig[k].view(np.int16)).to(dev) for k in range(nf)]
-    d_r = [torch.from_numpy(recon[k].view(np.int16)).to(dev) for k in range(nf)]
     eng = Engine(W, H, 0)
-    buf = np.zeros(32, np.uint64)
-
-    def run():
-        for poc in range(1, nf + 1):
-            eng.affine_me_poc(d_o[poc - 1], [d_r[r] for r in ref_list(poc)], lambda_for_poc(qp, poc), modes)
-        torch.cuda.synchronize()
-
-    run()
+    # bench.py's step at N = 1: the config's pairs in one vame_affine_me_batch call
+    n_pairs = sequence_pairs(nf) if cfg["scaling"] == "weak" else None
+    run = ShardRun(eng, W, H, qp, frames_for_pairs(n_pairs) if n_pairs else nf, modes, 1, 0, dev,
+                   n_pairs=n_pairs, streams=cfg["scaling"] == "weak")
+    buf = np.zeros(48, np.uint64)
+    run.step()
+    torch.cuda.synchronize()
     fn(buf.ctypes.data, 1)
     for _ in range(args.steps):
-        run()
+        run.step()
+    torch.cuda.synchronize()
     fn(buf.ctypes.data, 1)
     out = {}
-    for k, name in enumerate(("affine_me_quad", "affine_me_ctu")):
+    for k, name in enumerate(("affine_me_quad", "affine_me_ctu", "affine_me_half")):
         v = buf[16 * k:16 * k + 12].astype(np.float64)
         tot = v.sum()
+        if not tot:
+            continue
         e = {}
         for off, pas in ((0, "2cp"), (6, "3cp")):
-            e[pas] = {p: round(float(x / tot), 4) if tot else 0.0 for p, x in zip(PHASES, v[off:off + 6])}
+            e[pas] = {p: round(float(x / tot), 4) for p, x in zip(PHASES, v[off:off + 6])}
         e["wave_clock_total"] = float(tot)
         slot, life = float(buf[16 * k + 12]), float(buf[16 * k + 13])
         e["simd_slot_use"] = round(life / slot, 4) if slot else 0.0
         out[name] = e
-    print(json.dumps({"config": args.config, "steps": args.steps, "phases": out}, indent=1))
+    print(json.dumps({"config": args.config, "steps": args.steps, "pairs_per_step": run.pairs,
+                      "phases": out}, indent=1))
     eng.close()
 
 

@@ -824,13 +824,13 @@ const char* vame_strerror(int code) {
 const char* vame_last_hip_error(void) { return g_hip_err; }
 
 #if VAME_PHASE_TIMING
-// profiling-only builds: per-phase shader-clock sums [kernel][pass phase] (see vame_kernel.h)
-int vame_debug_phase_cycles(unsigned long long* out32, int reset) {
-  if (!out32) return VAME_E_INVALID;
+// profiling-only builds: per-phase shader-clock sums [kernel quad / ctu / half][pass phase] (see vame_kernel.h)
+int vame_debug_phase_cycles(unsigned long long* out48, int reset) {
+  if (!out48) return VAME_E_INVALID;
   VAME_HIP(hipDeviceSynchronize());
-  VAME_HIP(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 32));
+  VAME_HIP(hipMemcpyFromSymbol(out48, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 48));
   if (reset) {
-    unsigned long long z[32] = {};
+    unsigned long long z[48] = {};
     VAME_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)));
   }
   return VAME_OK;
