@@ -47,13 +47,19 @@ def test_version_and_errors():
     assert L.vame_cus_per_ctu(0) == 201 and L.vame_cus_per_ctu(1) == 284
 
 
+@pytest.mark.parametrize("tasks,chain,quad_items", [("8", "1", 36), ("8", "0", 44), ("4", "0", 72), ("1", "1", None)])
 @pytest.mark.parametrize("half128", [1, 0])
-def test_work_items_cover_every_cu_once(half128):
+def test_work_items_cover_every_cu_once(half128, tasks, chain, quad_items, monkeypatch):
     """The engine's work-item templates (vame_create's build_templates, run on
     the host without a device) partition the CTU's candidate CUs: every FULL
     (201) and HALF (284) output offset is covered by exactly one item's CU
     slot -- with the 128x64 / 64x128 CUs in 512-thread affine_me_half items
-    (one CU each, the default) or packed two per 1024-thread CTU item."""
+    (one CU each, the default) or packed two per 1024-thread CTU item, and
+    for every quadrant packing: autonomous items of 8 wave tasks (default),
+    4 or 1, the FULL 64x64 / 64x32 / 32x64 groups chained into one
+    cooperative item per quadrant (default) or one item each."""
+    monkeypatch.setenv("VAME_TASKS", tasks)
+    monkeypatch.setenv("VAME_CHAIN", chain)
     L = _lib.lib()
     items = (ctypes.c_int32 * 3)()
     for align, n in ((0, 201), (1, 284)):
@@ -61,7 +67,7 @@ def test_work_items_cover_every_cu_once(half128):
         assert L.vame_template_coverage(half128, align, hits, items) == 0
         assert list(hits) == [1] * n, (align, [i for i in range(n) if hits[i] != 1])
     quad, ctu, half = list(items)
-    assert quad > 0
+    assert quad > 0 and quad == (quad_items or quad)
     assert (ctu, half) == ((1, 4) if half128 else (3, 0))
 
 

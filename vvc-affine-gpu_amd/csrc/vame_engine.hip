@@ -105,72 +105,76 @@ struct CuDesc {
 
 int nsb_of(const CuDesc& c) { return c.w * c.h / 16; }
 
-void fill_slots(Item& it, const std::vector<CuDesc>& cus) {
-  if ((int)cus.size() > kMaxCu) abort();
-  it.nCu = (int16_t)cus.size();
-  int sb = 0;
-  for (size_t k = 0; k < cus.size(); k++) {
-    CuSlot& s = it.cu[k];
-    s.x = (int16_t)cus[k].x;
-    s.y = (int16_t)cus[k].y;
-    s.lw = (uint8_t)ilog2(cus[k].w);
-    s.lh = (uint8_t)ilog2(cus[k].h);
-    s.align = (uint8_t)cus[k].align;
-    s.outOff = (int16_t)cus[k].outOff;
-    s.sbBase = (int16_t)sb;
-    sb += nsb_of(cus[k]);
-  }
+void set_slot(CuSlot& s, const CuDesc& c, int sbBase) {
+  s.x = (int16_t)c.x;
+  s.y = (int16_t)c.y;
+  s.lw = (uint8_t)ilog2(c.w);
+  s.lh = (uint8_t)ilog2(c.h);
+  s.align = (uint8_t)c.align;
+  s.outOff = (int16_t)c.outOff;
+  s.sbBase = (int16_t)sbBase;
 }
 
-// Cooperative item: CUs of one size, each spanning nsb >= 64 lanes (one per
-// sub-block) of the workgroup (workgroup barriers per phase, LDS atomics).
-Item make_coop_item(int rx, int ry, const std::vector<CuDesc>& cus, int threads) {
+// Cooperative item: tasks of CUs of one size, each CU spanning nsb >= 64
+// lanes (one per sub-block) of the workgroup (workgroup barriers per phase,
+// LDS atomics), run one after another over the item's one staged tile.  A
+// single task holds slots 0 .. (up to kMaxCu), a chain's task t slots
+// t * kTaskCu ...
+Item make_coop_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& tasks, int threads) {
   Item it;
   memset(&it, 0, sizeof(it));
   it.rx = (int16_t)rx;
   it.ry = (int16_t)ry;
   it.coop = 1;
-  it.nWaves = kMaxWaves;
-  const int nsb = nsb_of(cus[0]);
-  for (auto& c : cus)
-    if (nsb_of(c) != nsb) abort();
-  if (nsb < 64 || (int)cus.size() * nsb > threads) abort();
-  it.logL = (int16_t)ilog2(nsb);
-  fill_slots(it, cus);
+  if (tasks.empty() || (int)tasks.size() > kMaxTasks) abort();
+  it.nTasks = (int16_t)tasks.size();
+  const int stride = tasks.size() > 1 ? kTaskCu : kMaxCu;
+  for (size_t t = 0; t < tasks.size(); t++) {
+    const int nsb = nsb_of(tasks[t][0]);
+    const int n = (int)tasks[t].size();
+    for (auto& c : tasks[t])
+      if (nsb_of(c) != nsb) abort();
+    if (nsb < 64 || n * nsb > threads || n > stride) abort();
+    for (int i = 0; i < n; i++) set_slot(it.cu[t * stride + i], tasks[t][i], i * nsb);
+    it.cu[t * stride].task = n | (ilog2(nsb) << 8);
+    it.nCu = (int16_t)(t * stride + n);
+  }
   return it;
 }
+Item make_coop_item(int rx, int ry, const std::vector<CuDesc>& cus, int threads) {
+  return make_coop_item(rx, ry, std::vector<std::vector<CuDesc>>{cus}, threads);
+}
 
-// Autonomous item: up to 4 waves, each holding CUs of ONE size (<= 64
-// sub-blocks, one lane per sub-block), so a wave's segment size is uniform.
-Item make_auto_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& waves) {
+// Autonomous item: up to kMaxTasks wave tasks, each CUs of ONE size (<= 64
+// sub-blocks, one lane per sub-block), so a task's segment size is uniform.
+// Wave w runs tasks w, w + 4, ... over the one staged tile: task t holds CU
+// slots t * kTaskCu .. (its first slot carries the task's CU count and lanes
+// per CU) and the wave's prediction rows (t % 4) * 64 ...  Unused slots stay
+// zero (lw 0).
+Item make_auto_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& tasks) {
   Item it;
   memset(&it, 0, sizeof(it));
   it.rx = (int16_t)rx;
   it.ry = (int16_t)ry;
   it.coop = 0;
-  if (waves.empty() || (int)waves.size() > kMaxWaves) abort();
-  it.nWaves = (int16_t)waves.size();
-  std::vector<CuDesc> all;
-  for (size_t w = 0; w < waves.size(); w++) {
-    const int nsb = nsb_of(waves[w][0]);
-    int used = 0;
-    for (auto& c : waves[w]) {
+  if (tasks.empty() || (int)tasks.size() > kMaxTasks) abort();
+  it.nTasks = (int16_t)tasks.size();
+  it.nCu = (int16_t)(tasks.size() * kTaskCu);
+  for (size_t t = 0; t < tasks.size(); t++) {
+    const int nsb = nsb_of(tasks[t][0]);
+    const int n = (int)tasks[t].size();
+    for (auto& c : tasks[t])
       if (nsb_of(c) != nsb) abort();
-      used += nsb;
-    }
-    if (used > 64 || nsb < 16) abort();  // the kernel's segment sums handle 16 / 32 / 64
-    it.wave[w].cuBegin = (int16_t)all.size();
-    all.insert(all.end(), waves[w].begin(), waves[w].end());
-    it.wave[w].cuEnd = (int16_t)all.size();
-    it.wave[w].logL = (int16_t)ilog2(nsb);
+    if (n * nsb > 64 || nsb < 16 || n > kTaskCu) abort();  // the kernel's segment sums handle 16 / 32 / 64
+    for (int i = 0; i < n; i++) set_slot(it.cu[t * kTaskCu + i], tasks[t][i], (int)(t % 4) * 64 + i * nsb);
+    it.cu[t * kTaskCu].task = n | (ilog2(nsb) << 8);
   }
-  fill_slots(it, all);
   return it;
 }
 
-// CUs of one quadrant and one alignment, <= 64 sub-blocks: waves of one size
-// class (largest first), then items of 4 consecutive waves.
-void pack_autonomous(int qx, int qy, std::vector<CuDesc> cus, std::vector<Item>& out) {
+// CUs of one quadrant and one alignment, <= 64 sub-blocks: wave tasks of one
+// size class (largest first), then items of `perItem` consecutive tasks.
+void pack_autonomous(int qx, int qy, std::vector<CuDesc> cus, std::vector<Item>& out, int perItem) {
   std::stable_sort(cus.begin(), cus.end(),
                    [](const CuDesc& a, const CuDesc& b) { return nsb_of(a) > nsb_of(b); });
   std::vector<std::vector<CuDesc>> waves;
@@ -180,9 +184,9 @@ void pack_autonomous(int qx, int qy, std::vector<CuDesc> cus, std::vector<Item>&
       waves.push_back({});
     waves.back().push_back(c);
   }
-  for (size_t w = 0; w < waves.size(); w += kMaxWaves) {
+  for (size_t w = 0; w < waves.size(); w += perItem) {
     std::vector<std::vector<CuDesc>> grp(waves.begin() + w,
-                                         waves.begin() + std::min(waves.size(), w + kMaxWaves));
+                                         waves.begin() + std::min(waves.size(), w + perItem));
     out.push_back(make_auto_item(qx, qy, grp));
   }
 }
@@ -193,11 +197,13 @@ void pack_autonomous(int qx, int qy, std::vector<CuDesc> cus, std::vector<Item>&
 //   half     : with `half`, each 128x64 / 64x128 CU alone, its own region
 //              (affine_me_half, 512 threads)
 //   quadFull : FULL groups <= 64x64 per 64x64 quadrant: 64x64 / 64x32 / 32x64
-//              cooperative (one item per group), the rest autonomous
+//              cooperative (one item chaining the three groups, or with
+//              `chainCoop` off one item per group), the rest autonomous in
+//              items of `tasks` wave tasks
 //   quadHalf : HALF groups per quadrant (no HALF CU crosses a quadrant):
 //              64x32 + 32x64 cooperative, the rest autonomous
 void build_templates(std::vector<Item>& big, std::vector<Item>& halfItems, std::vector<Item>& quadFull,
-                     std::vector<Item>& quadHalf, bool half) {
+                     std::vector<Item>& quadHalf, bool half, int tasks, bool chainCoop) {
   for (int g = 0; g < kFullGroups; g++) {
     const int w = kFullW[g], h = kFullH[g], n = (kCtu * kCtu) / (w * h), cols = kCtu / w;
     if (w == 128 || h == 128) {
@@ -220,6 +226,7 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& halfItems, std::
     const int qx = (q & 1) * 64, qy = (q >> 1) * 64;
     auto inq = [&](int x, int y) { return x >= qx && x < qx + 64 && y >= qy && y < qy + 64; };
     std::vector<CuDesc> small;
+    std::vector<std::vector<CuDesc>> chain;
     for (int g = 0; g < kFullGroups; g++) {
       const int w = kFullW[g], h = kFullH[g], n = (kCtu * kCtu) / (w * h), cols = kCtu / w;
       if (w == 128 || h == 128) continue;
@@ -228,12 +235,15 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& halfItems, std::
         const int x = (k % cols) * w, y = (k / cols) * h;
         if (inq(x, y)) c.push_back({x, y, w, h, 0, kFullStride[g] + k});
       }
-      if (w * h / 16 > 64)
-        quadFull.push_back(make_coop_item(qx, qy, c, Cfg<kKindQuad>::THREADS));
-      else
+      if (w * h / 16 <= 64)
         small.insert(small.end(), c.begin(), c.end());
+      else if (chainCoop)
+        chain.push_back(c);
+      else
+        quadFull.push_back(make_coop_item(qx, qy, c, Cfg<kKindQuad>::THREADS));
     }
-    pack_autonomous(qx, qy, small, quadFull);
+    if (!chain.empty()) quadFull.push_back(make_coop_item(qx, qy, chain, Cfg<kKindQuad>::THREADS));
+    pack_autonomous(qx, qy, small, quadFull, tasks);
     std::vector<CuDesc> bigHalf;
     small.clear();
     for (int g = 0; g < kHalfGroups; g++)
@@ -245,7 +255,7 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& halfItems, std::
         (nsb_of(c) > 64 ? bigHalf : small).push_back(c);
       }
     if (!bigHalf.empty()) quadHalf.push_back(make_coop_item(qx, qy, bigHalf, Cfg<kKindQuad>::THREADS));
-    pack_autonomous(qx, qy, small, quadHalf);
+    pack_autonomous(qx, qy, small, quadHalf, tasks);
   }
 }
 
@@ -370,6 +380,11 @@ int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e && *e ? atoi(e) : dflt;
 }
+
+// wave tasks per autonomous quadrant item (VAME_TASKS, 1..8)
+int tasks_per_item() { return std::min(kMaxTasks, std::max(1, env_int("VAME_TASKS", 8))); }
+// one cooperative item per quadrant for the FULL 64x64 / 64x32 / 32x64 groups (VAME_CHAIN)
+bool chain_coop() { return env_int("VAME_CHAIN", 1) != 0; }
 
 // The kernel instance of a launch mode (vame_kernel.h MODE: 1 = 2-CP only,
 // 2 = 3-CP only, 3 = 2-CP then 3-CP).
@@ -586,10 +601,11 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   DeviceGuard guard(device);
   VAME_HIP(guard.err);
   std::vector<Item> big3, big1, hf, qf, qh, unused;
-  build_templates(big3, unused, qf, qh, false);
+  const int tasks = tasks_per_item();
+  build_templates(big3, unused, qf, qh, false, tasks, chain_coop());
   qf.clear();
   qh.clear();
-  build_templates(big1, hf, qf, qh, true);
+  build_templates(big1, hf, qf, qh, true, tasks, chain_coop());
   vame_ctx* c = new vame_ctx();
   c->device = device;
   c->W = width;
@@ -692,14 +708,14 @@ int vame_affine_me(vame_ctx* c, const uint16_t* ref, const uint16_t* cur, float 
 int vame_template_coverage(int half128, int align, int32_t* hits, int32_t* items3) {
   if (!hits || (align != 0 && align != 1)) return VAME_E_INVALID;
   std::vector<Item> big, hf, qf, qh;
-  build_templates(big, hf, qf, qh, half128 != 0);
+  build_templates(big, hf, qf, qh, half128 != 0, tasks_per_item(), chain_coop());
   const int n = align ? kHalfCusPerCtu : kFullCusPerCtu;
   for (int i = 0; i < n; i++) hits[i] = 0;
   for (const auto* v : {&big, &hf, &qf, &qh})
     for (const Item& it : *v)
       for (int k = 0; k < it.nCu; k++) {
         const CuSlot& s = it.cu[k];
-        if (s.align != align) continue;
+        if (s.lw == 0 || s.align != align) continue;  // lw 0: an unused slot
         if (s.outOff < 0 || s.outOff >= n) return VAME_E_INVALID;
         hits[s.outOff]++;
       }

@@ -38,8 +38,10 @@
 
 namespace vame {
 
-constexpr int kMaxCu = 16;    // CU slots per work item
-constexpr int kMaxWaves = 4;
+constexpr int kMaxCu = 16;    // CU state slots per workgroup (LDS)
+constexpr int kMaxTasks = 8;  // autonomous items: wave tasks (wave w runs tasks w, w + 4)
+constexpr int kTaskCu = 4;    // CUs per wave task (<= 64 sub-blocks, >= 16 each)
+constexpr int kItemCu = kMaxTasks * kTaskCu;  // CU slots per work item
 constexpr int kThreads = 256;  // quadrant workgroups
 constexpr int kNumMom = 24;   // 3 CP: {1,u,v,uu,uv,vv} x {xx,xy,yy} + {1,u,v} x {xe,ye}
 constexpr int kNumVal2 = 14;  // 2 CP: 10 distinct matrix entries + 4 right-hand sides
@@ -55,25 +57,23 @@ struct CuSlot {     // 16 bytes
   uint8_t align;    // 0 FULL, 1 HALF
   uint8_t pad0;
   int16_t outOff;   // RETURN_STRIDE[group] + cuIdx
-  int16_t sbBase;   // first sub-block of this CU inside the item (prediction buffer / 16)
-  int32_t pad1;
+  int16_t sbBase;   // first sub-block of this CU inside the workgroup (prediction rows)
+  int32_t task;     // a task's first slot: CUs in the task | log2 lanes per CU << 8
 };
 
-struct WaveDesc {   // autonomous items: the CU slots a wave owns, all of one size
-  int16_t cuBegin, cuEnd;
-  int16_t logL;     // log2 lanes per CU (= sub-blocks per CU)
-  int16_t pad;
-};
-
+// An item's CUs come in tasks of one CU size each, run over the item's one
+// staged tile: a cooperative item's tasks one after another by the whole
+// workgroup, an autonomous item's tasks by its waves (wave w: tasks w, w + 4).
+// Task t holds CU slots t * kTaskCu .. (a single-task cooperative item: up to
+// kMaxCu slots from 0).
 struct Item {
-  int16_t nCu;      // CU slots
+  int16_t nCu;      // CU slots (host view; unused slots have lw 0)
   int16_t rx, ry;   // region origin (CTU-relative)
-  int16_t coop;     // 1: cooperative (CUs span waves, all CUs of one size)
-  int16_t nWaves;   // autonomous: waves holding CUs
-  int16_t logL;     // cooperative: log2 lanes per CU (>= 6)
+  int16_t coop;     // 1: cooperative (a task's CUs span waves)
+  int16_t nTasks;
   int16_t rw, rh;   // affine_me_half items: the region's extent (the CU's); 0 elsewhere
-  WaveDesc wave[kMaxWaves];
-  CuSlot cu[kMaxCu];
+  int16_t pad;
+  CuSlot cu[kItemCu];
 };
 
 // One (POC, refIdx) pair of a launch: the reference's kernel arguments for it
@@ -1152,7 +1152,9 @@ template <int KIND>
 struct Cfg {
   static constexpr int REGION = KIND == kKindQuad ? 64 : 128;  // largest region edge
   static constexpr int THREADS = KIND == kKindQuad ? 256 : KIND == kKindCtu ? 1024 : 512;  // = sub-blocks
-  static constexpr int MAXCU = KIND == kKindHalf ? 1 : kMaxCu;  // CU slots per item
+  static constexpr int MAXCU = KIND == kKindHalf ? 1 : kMaxCu;  // CU state slots (LDS)
+  static constexpr int ITEMCU = KIND == kKindQuad ? kItemCu : MAXCU;  // CU slots per item
+  static constexpr bool AUTO = KIND == kKindQuad;       // holds autonomous items
   static constexpr int MARGIN = 16;                     // reference-tile margin (samples)
   static constexpr int TILE = REGION + 2 * MARGIN;      // tile edge (samples)
   // tile pitch (samples) == 8 (mod 16): the window rows of sub-blocks 4 rows
@@ -1481,8 +1483,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
   __shared__ uint8_t s_eqmap[80];
   __shared__ CuState s_st[C::MAXCU];
-  __shared__ CuSlot s_cu[C::MAXCU];
-  __shared__ WaveDesc s_wave[kMaxWaves];
+  __shared__ CuSlot s_cu[C::ITEMCU];
   __shared__ int s_hdr[4];
   __shared__ long long s_dup[(VAME_DUP & 4) ? kNumMom : 1];
 
@@ -1571,11 +1572,10 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       }
     }
   }
-  if (tid < C::MAXCU) s_cu[tid] = it->cu[tid];
-  if (tid < kMaxWaves) s_wave[tid] = it->wave[tid];
+  if (tid < C::ITEMCU) s_cu[tid] = it->cu[tid];
   if (tid < 48) s_coef[tid] = reinterpret_cast<const uint4*>(&kCoefTab)[tid];
   if (tid < 80) s_eqmap[tid] = kEqMap.v[tid];
-  if (tid == 0) s_hdr[0] = it->nCu | (it->coop << 8) | (it->nWaves << 16) | (it->logL << 24);
+  if (tid == 0) s_hdr[0] = it->coop | (it->nTasks << 16);
   for (int i = tid; i < C::MAXCU * kNumMom; i += C::THREADS) (&s_val[0][0])[i] = 0;
   PH_INIT
   if (!regionOut) {
@@ -1588,419 +1588,430 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   __syncthreads();
   PH_START
   const int hdr = __builtin_amdgcn_readfirstlane(s_hdr[0]);
-  const int nCu = hdr & 0xFF, nWaves = (hdr >> 16) & 0xFF;
-  const bool coop = ((hdr >> 8) & 0xFF) != 0;
+  const int nTasks = (hdr >> 16) & 0xFF;
+  const bool coop = !C::AUTO || (hdr & 0xFF) != 0;
   PH_MARK(kPhStage)
-  if (!coop && wv >= nWaves) {  // wave-uniform: an autonomous wave without CUs
+  if (!coop && wv >= nTasks) {  // wave-uniform: an autonomous wave without CUs
     PH_FLUSH
     return;
   }
 
-  // ---- CUs of this wave, this lane's CU and sub-blocks (fixed for the item)
-  int cuB, cuE, logL, lidx;
-  if (coop) {
-    cuB = 0;
-    cuE = nCu;
-    logL = (hdr >> 24) & 0xFF;
-    lidx = tid;
-  } else {
-    const WaveDesc wd = s_wave[wv];
-    cuB = wd.cuBegin;
-    cuE = wd.cuEnd;
-    logL = wd.logL;
-    lidx = lane;
-  }
-  cuB = __builtin_amdgcn_readfirstlane(cuB);
-  cuE = __builtin_amdgcn_readfirstlane(cuE);
-  logL = __builtin_amdgcn_readfirstlane(logL);
-  const int logS = min(logL, 6);                       // segment = lanes of one CU in one wave
-  const int nCuW = coop ? (wv == 0 ? nCu : 0) : cuE - cuB;  // lanes doing per-CU work
-  const int kLane = cuB + (lidx >> logL);
-  const int myCu = kLane < cuE ? kLane : -1;
-  Geo g;
-  g.x = g.y = g.lw = g.lh = g.w = g.h = 0;
-  const int local = lidx & ((1 << logL) - 1);  // this lane's sub-block (raster order in its CU)
-  int sbIdx = 0, sx = 0, sy = 0, sbCols = 1;
-  bool active = false;
-  if (myCu >= 0) {
-    const CuSlot cs = s_cu[myCu];
-    g.lw = cs.lw;
-    g.lh = cs.lh;
-    g.w = 1 << g.lw;
-    g.h = 1 << g.lh;
-    g.x = ctuX + cs.x;
-    g.y = ctuY + cs.y;
-    sbIdx = cs.sbBase + local;
-    sbCols = 1 << (g.lw - 2);
-    sx = (local & (sbCols - 1)) << 2;
-    sy = (local >> (g.lw - 2)) << 2;
-    active = (g.x + g.w <= W) && (g.y + g.h <= H);  // affine.cl:192-193
-  }
-  const bool leader = myCu >= 0 && (lane & ((1 << logS) - 1)) == (1 << logS) - 1;
+  // Tasks over the one staged tile: a cooperative item's tasks one after
+  // another, an autonomous wave's tasks wv, wv + 4, ...  Each task's CU slots
+  // are first moved into slots 0 .. (cooperative) or the wave's own slots
+  // wv * kTaskCu .. (autonomous: its CU state, moments and systems; its
+  // sub-blocks use the wave's own prediction rows, so its tasks need no
+  // workgroup barrier).
+  const int tstep = coop ? 1 : 4;
+  for (int task = coop ? 0 : __builtin_amdgcn_readfirstlane(wv);; task += tstep) {
+    // ---- CUs of this wave, this lane's CU and sub-blocks (fixed for the task)
+    const int lidx = coop ? tid : lane;
+    const int ti = s_cu[coop ? 0 : wv * kTaskCu].task;
+    int cuB = coop ? 0 : wv * kTaskCu;
+    int cuE = cuB + (ti & 0xFF);
+    int logL = (ti >> 8) & 0xFF;
+    cuB = __builtin_amdgcn_readfirstlane(cuB);
+    cuE = __builtin_amdgcn_readfirstlane(cuE);
+    logL = __builtin_amdgcn_readfirstlane(logL);
+    const int logS = min(logL, 6);                       // segment = lanes of one CU in one wave
+    const int nCuW = coop ? (wv == 0 ? cuE : 0) : cuE - cuB;  // lanes doing per-CU work
+    const int kLane = cuB + (lidx >> logL);
+    const int myCu = kLane < cuE ? kLane : -1;
+    Geo g;
+    g.x = g.y = g.lw = g.lh = g.w = g.h = 0;
+    const int local = lidx & ((1 << logL) - 1);  // this lane's sub-block (raster order in its CU)
+    int sbIdx = 0, sx = 0, sy = 0, sbCols = 1;
+    bool active = false;
+    if (myCu >= 0) {
+      const CuSlot cs = s_cu[myCu];
+      g.lw = cs.lw;
+      g.lh = cs.lh;
+      g.w = 1 << g.lw;
+      g.h = 1 << g.lh;
+      g.x = ctuX + cs.x;
+      g.y = ctuY + cs.y;
+      sbIdx = cs.sbBase + local;
+      sbCols = 1 << (g.lw - 2);
+      sx = (local & (sbCols - 1)) << 2;
+      sy = (local >> (g.lw - 2)) << 2;
+      active = (g.x + g.w <= W) && (g.y + g.h <= H);  // affine.cl:192-193
+    }
+    const bool leader = myCu >= 0 && (lane & ((1 << logS) - 1)) == (1 << logS) - 1;
 
-  // one copy of the pass per CP count and item class: ncp and coop are
-  // compile-time constants in each, so the 2-CP pass carries none of the 3-CP
-  // selects and branches, and each copy keeps its spills outside its loops
-  auto run_pass = [&](auto ncpTag, auto coopTag, auto keepTag) {
-    constexpr int ncp = decltype(ncpTag)::value;
-    constexpr bool coop = decltype(coopTag)::value;
-    constexpr bool keepS = decltype(keepTag)::value;  // 2-CP pass that feeds a 3-CP pass
-    constexpr int ph_off = ncp == 3 ? kNumPhases : 0;
-    (void)ph_off;
-    constexpr int kDup = (VAME_DUP & 32) && ncp != 3 ? 0 : VAME_DUP;  // timing-only builds
-    const int niter = (ncp == 3 ? 4 : 5) + p.extra;
+    // one copy of the pass per CP count and item class: ncp and coop are
+    // compile-time constants in each, so the 2-CP pass carries none of the 3-CP
+    // selects and branches, and each copy keeps its spills outside its loops
+    auto run_pass = [&](auto ncpTag, auto coopTag, auto keepTag) {
+      constexpr int ncp = decltype(ncpTag)::value;
+      constexpr bool coop = decltype(coopTag)::value;
+      constexpr bool keepS = decltype(keepTag)::value;  // 2-CP pass that feeds a 3-CP pass
+      constexpr int ph_off = ncp == 3 ? kNumPhases : 0;
+      (void)ph_off;
+      constexpr int kDup = (VAME_DUP & 32) && ncp != 3 ? 0 : VAME_DUP;  // timing-only builds
+      const int niter = (ncp == 3 ? 4 : 5) + p.extra;
 
-    // ---- per-CU initial CPMVs (2 CP: zero; 3 CP: derived from the 2-CP winner)
-    if (lane < nCuW) {
-      int k = __lane_id();  // == lane, recomputed: not a spilled loop-carried copy
-      opaque(k);
-      k += cuB;
-      const CuSlot cs = s_cu[k];
-      CuState& st = s_st[k];
-      const int cx = ctuX + cs.x, cy = ctuY + cs.y;
-      int c[6] = {0, 0, 0, 0, 0, 0};
-      if (ncp == 3) {
-        int prev[4];
-        if (run2) {
-          for (int i = 0; i < 4; i++) prev[i] = st.best[i];
+      // ---- per-CU initial CPMVs (2 CP: zero; 3 CP: derived from the 2-CP winner)
+      if (lane < nCuW) {
+        int k = __lane_id();  // == lane, recomputed: not a spilled loop-carried copy
+        opaque(k);
+        k += cuB;
+        const CuSlot cs = s_cu[k];
+        CuState& st = s_st[k];
+        const int cx = ctuX + cs.x, cy = ctuY + cs.y;
+        int c[6] = {0, 0, 0, 0, 0, 0};
+        if (ncp == 3) {
+          int prev[4];
+          if (run2) {
+            for (int i = 0; i < 4; i++) prev[i] = st.best[i];
+          } else {
+            const vame_cpmvs_dev& pv =
+                p.prev[cs.align][(size_t)ctu * (cs.align ? kHalfCusPerCtu : kFullCusPerCtu) + cs.outOff];
+            prev[0] = pv.ltx; prev[1] = pv.lty; prev[2] = pv.rtx; prev[3] = pv.rty;
+          }
+          // affine.cl:81-105
+          const int sh = 7 + cs.lh - cs.lw;
+          int vx2 = shl(prev[0], 7) - shl(prev[3] - prev[1], sh);
+          int vy2 = shl(prev[1], 7) + shl(prev[2] - prev[0], sh);
+          vx2 = (vx2 + 64 - (vx2 >= 0)) >> 7;
+          vy2 = (vy2 + 64 - (vy2 >= 0)) >> 7;
+          int lbx = clampi(vx2, -(1 << 17), (1 << 17) - 1);
+          int lby = clampi(vy2, -(1 << 17), (1 << 17) - 1);
+          lbx = shl(to_quarter(lbx), 2);
+          lby = shl(to_quarter(lby), 2);
+          clip_mv(lbx, lby, cx, cy, W, H);
+          c[0] = prev[0]; c[1] = prev[1]; c[2] = prev[2]; c[3] = prev[3]; c[4] = lbx; c[5] = lby;
+          // Seed reuse (exact): when the derived LB reproduces the 2-CP motion
+          // field -- (LB - LT) << (7 - log2 h) == (-(RT - LT).y, (RT - LT).x)
+          // << (7 - log2 w), i.e. no rounding or clipping in the derivation
+          // (always so for square CUs) -- iteration 0's MV field, spread test,
+          // prediction and gradients are those of the 2-CP winner, whose SATD
+          // and per-sub-block gradient sums the 2-CP pass kept.  Iteration 0
+          // then only re-prices the rate and rebuilds the 6-parameter equations.
+          int skip = 0, satd0 = 0;
+          if (run2 && st.bestHasS) {
+            const int hx = shl(prev[2] - prev[0], 7 - cs.lw), hy = shl(prev[3] - prev[1], 7 - cs.lw);
+            const int vx = shl(lbx - prev[0], 7 - cs.lh), vy = shl(lby - prev[1], 7 - cs.lh);
+            if (vx == -hy && vy == hx) {
+              skip = 1;
+              satd0 = st.bestSatd;
+            }
+          }
+          st.seedSkip = skip;
+          st.satd = satd0;
         } else {
-          const vame_cpmvs_dev& pv =
-              p.prev[cs.align][(size_t)ctu * (cs.align ? kHalfCusPerCtu : kFullCusPerCtu) + cs.outOff];
-          prev[0] = pv.ltx; prev[1] = pv.lty; prev[2] = pv.rtx; prev[3] = pv.rty;
+          st.satd = 0;
+          st.bestHasS = 0;
         }
-        // affine.cl:81-105
-        const int sh = 7 + cs.lh - cs.lw;
-        int vx2 = shl(prev[0], 7) - shl(prev[3] - prev[1], sh);
-        int vy2 = shl(prev[1], 7) + shl(prev[2] - prev[0], sh);
-        vx2 = (vx2 + 64 - (vx2 >= 0)) >> 7;
-        vy2 = (vy2 + 64 - (vy2 >= 0)) >> 7;
-        int lbx = clampi(vx2, -(1 << 17), (1 << 17) - 1);
-        int lby = clampi(vy2, -(1 << 17), (1 << 17) - 1);
-        lbx = shl(to_quarter(lbx), 2);
-        lby = shl(to_quarter(lby), 2);
-        clip_mv(lbx, lby, cx, cy, W, H);
-        c[0] = prev[0]; c[1] = prev[1]; c[2] = prev[2]; c[3] = prev[3]; c[4] = lbx; c[5] = lby;
-        // Seed reuse (exact): when the derived LB reproduces the 2-CP motion
-        // field -- (LB - LT) << (7 - log2 h) == (-(RT - LT).y, (RT - LT).x)
-        // << (7 - log2 w), i.e. no rounding or clipping in the derivation
-        // (always so for square CUs) -- iteration 0's MV field, spread test,
-        // prediction and gradients are those of the 2-CP winner, whose SATD
-        // and per-sub-block gradient sums the 2-CP pass kept.  Iteration 0
-        // then only re-prices the rate and rebuilds the 6-parameter equations.
-        int skip = 0, satd0 = 0;
-        if (run2 && st.bestHasS) {
-          const int hx = shl(prev[2] - prev[0], 7 - cs.lw), hy = shl(prev[3] - prev[1], 7 - cs.lw);
-          const int vx = shl(lbx - prev[0], 7 - cs.lh), vy = shl(lby - prev[1], 7 - cs.lh);
-          if (vx == -hy && vy == hx) {
-            skip = 1;
-            satd0 = st.bestSatd;
-          }
+        // fresh constants (opaque): as loop-carried values the compiler kept
+        // them in spill slots, whose scratch traffic reached HBM
+        int never = (int)0x80000000;  // outside the clamped CPMV range: never matches
+        int costInit = (int)kCostInit;
+        opaque(never);
+        opaque(costInit);
+        for (int i = 0; i < 6; i++) {
+          st.cur[i] = c[i];
+          st.prev[i] = never;
+          st.best[i] = c[i];
         }
-        st.seedSkip = skip;
-        st.satd = satd0;
-      } else {
-        st.satd = 0;
-        st.bestHasS = 0;
+        st.bestCost = (long long)costInit;
+        st.bestCostSnap = (long long)costInit;
+        st.rate = affine_bits(c, ncp);
+        st.inframe = (cx + (1 << cs.lw) <= W) && (cy + (1 << cs.lh) <= H);
+        st.live = st.inframe;
       }
-      // fresh constants (opaque): as loop-carried values the compiler kept
-      // them in spill slots, whose scratch traffic reached HBM
-      int never = (int)0x80000000;  // outside the clamped CPMV range: never matches
-      int costInit = (int)kCostInit;
-      opaque(never);
-      opaque(costInit);
-      for (int i = 0; i < 6; i++) {
-        st.cur[i] = c[i];
-        st.prev[i] = never;
-        st.best[i] = c[i];
-      }
-      st.bestCost = (long long)costInit;
-      st.bestCostSnap = (long long)costInit;
-      st.rate = affine_bits(c, ncp);
-      st.inframe = (cx + (1 << cs.lw) <= W) && (cy + (1 << cs.lh) <= H);
-      st.live = st.inframe;
-    }
-    phase_sync(coop);
+      phase_sync(coop);
 
-    for (int iter = 0; iter <= niter; iter++) {
-      // =============== prediction + SATD (affine.cl:208-393) ===============
-      // Everything a lane produces here is only read while its CU is live
-      // (the CU's lanes are uniformly live or not), so the whole step runs
-      // under `live`: the DPP neighbour reads at the CU's edges may see lanes
-      // of other CUs, whose columns the border replication discards.
-      uint2 Pr[4], Og[4];  // this lane's prediction and original rows (packed pairs)
-      uint4 X[6];          // extended rows 0..3 (X[1..4]) and the neighbours' edges
-      const bool live = active && s_st[myCu < 0 ? 0 : myCu].live;
-      // 3-CP iteration 0 of a seed-reuse CU: SATD (set at init) and gradient
-      // sums come from the 2-CP pass
-      const bool reuse = ncp == 3 && iter == 0 && s_st[myCu < 0 ? 0 : myCu].seedSkip;
-      if (live && !reuse && !(VAME_ABLATE & 8)) {
-        PC_ADD
-        Geo gp = g;
-        int sxp = sx, syp = sy;
-        opaque_geo(gp, sxp, syp);  // recomputed per phase (not hoisted: VGPRs)
-        int cp[6];
-        for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
-        const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
-        bool outside;
-        const int satdLane = predict_sb<C::TILE, C::TP, PROF, (VAME_ABLATE & 1024) != 0 && ncp == 3>(
-            f, sxp, syp, gp, s_tile, tx0, ty0, tileW - 9, tileH - 9, ref, cur, W, H, s_coef, Pr, Og, outside);
+      for (int iter = 0; iter <= niter; iter++) {
+        // =============== prediction + SATD (affine.cl:208-393) ===============
+        // Everything a lane produces here is only read while its CU is live
+        // (the CU's lanes are uniformly live or not), so the whole step runs
+        // under `live`: the DPP neighbour reads at the CU's edges may see lanes
+        // of other CUs, whose columns the border replication discards.
+        uint2 Pr[4], Og[4];  // this lane's prediction and original rows (packed pairs)
+        uint4 X[6];          // extended rows 0..3 (X[1..4]) and the neighbours' edges
+        const bool live = active && s_st[myCu < 0 ? 0 : myCu].live;
+        // 3-CP iteration 0 of a seed-reuse CU: SATD (set at init) and gradient
+        // sums come from the 2-CP pass
+        const bool reuse = ncp == 3 && iter == 0 && s_st[myCu < 0 ? 0 : myCu].seedSkip;
+        if (live && !reuse && !(VAME_ABLATE & 8)) {
+          PC_ADD
+          Geo gp = g;
+          int sxp = sx, syp = sy;
+          opaque_geo(gp, sxp, syp);  // recomputed per phase (not hoisted: VGPRs)
+          int cp[6];
+          for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
+          const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
+          bool outside;
+          const int satdLane = predict_sb<C::TILE, C::TP, PROF, (VAME_ABLATE & 1024) != 0 && ncp == 3>(
+              f, sxp, syp, gp, s_tile, tx0, ty0, tileW - 9, tileH - 9, ref, cur, W, H, s_coef, Pr, Og, outside);
 #if VAME_COUNT_PRED
-        {  // instrumentation: windows outside the tile, per kernel and pass, one atomic per wave
-          const unsigned long long out = __builtin_amdgcn_ballot_w64(outside);
-          if (out && __lane_id() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
-            atomicAdd(&g_pred_count[2 + 2 * (REGION == 128) + (ncp == 3)], (unsigned long long)__popcll(out));
-        }
+          {  // instrumentation: windows outside the tile, per kernel and pass, one atomic per wave
+            const unsigned long long out = __builtin_amdgcn_ballot_w64(outside);
+            if (out && __lane_id() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
+              atomicAdd(&g_pred_count[2 + 2 * (REGION == 128) + (ncp == 3)], (unsigned long long)__popcll(out));
+          }
 #endif
-        if (kDup & 1) {
-          MvField f2 = f;
-          opaque(f2.bx);
-          uint2 P2[4], O2[4];
-          bool out2;
-          int s2 = predict_sb<C::TILE, C::TP, PROF>(f2, sxp, syp, gp, s_tile, tx0, ty0, tileW - 9, tileH - 9,
-                                                    ref, cur, W, H, s_coef, P2, O2, out2);
-          s2 += (int)(P2[0].x ^ P2[3].y ^ O2[1].x);
-          asm volatile("" ::"v"(s2));
-        }
-        // extended rows (neighbour columns by DPP), edge rows published for
-        // the sub-blocks above and below
+          if (kDup & 1) {
+            MvField f2 = f;
+            opaque(f2.bx);
+            uint2 P2[4], O2[4];
+            bool out2;
+            int s2 = predict_sb<C::TILE, C::TP, PROF>(f2, sxp, syp, gp, s_tile, tx0, ty0, tileW - 9, tileH - 9,
+                                                      ref, cur, W, H, s_coef, P2, O2, out2);
+            s2 += (int)(P2[0].x ^ P2[3].y ^ O2[1].x);
+            asm volatile("" ::"v"(s2));
+          }
+          // extended rows (neighbour columns by DPP), edge rows published for
+          // the sub-blocks above and below
 #pragma unroll
-        for (int r = 0; r < 4; r++)
-          X[r + 1] = ext_row(Pr[r], dpp32<0x138, 0xF>((int)Pr[r].y), dpp32<0x130, 0xF>((int)Pr[r].x));
-        s_top[sbIdx] = Pr[0];
-        s_bot[sbIdx] = Pr[3];
-        const int v = logS == 4 ? seg_sum_c<4>(satdLane)
-                      : logS == 5 ? seg_sum_c<5>(satdLane) : seg_sum_c<6>(satdLane);
-        if (leader) {
-          if (coop)
-            atomicAdd(&s_st[myCu].satd, v);
-          else
-            s_st[myCu].satd = v;
-        }
-      }
-      phase_sync(coop);
-      PH_MARK(kPhPredict)
-
-      // =============== cost, best update (affine.cl:416-457) ===============
-      // The cost is the SATD sum plus floor(lambda * (bits + 2)), the rate
-      // bits of the current CPMVs (calc_affine_bits, aux_functions.cl:2140-
-      // 2189) kept in CuState by the update step; the strict best is kept.
-      const bool lastIter = iter == niter;
-      bool better = false;  // keepS: this lane's CU improved
-      if constexpr (!keepS) {
-        // the CU's lane 7 prices and keeps the best; lanes 0-5 copy the CPMVs
-        int bet = 0;
-        if (myCu >= 0 && local == 7) {
-          CuState& st = s_st[myCu];
-          if (iter == 0 || st.live) {
-            const float prod = __fmul_rn(pa.lambda, (float)(st.rate + kRuiBits));
-            const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
-            if (cost < st.bestCost) {
-              st.bestCost = cost;
-              bet = 1;
-            }
-          }
-          st.satd = 0;
-        }
-        bet = __builtin_amdgcn_update_dpp(0, bet, 0x157, 0xF, 0xF, false);  // row_newbcast:7
-        if (myCu >= 0 && local < 6 && bet) s_st[myCu].best[local] = s_st[myCu].cur[local];
-      } else {
-        // 2-CP pass followed by a 3-CP pass: every lane of the CU prices it, so
-        // each knows whether its CU improved and keeps its gradient sums for
-        // the 3-CP seed reuse.  The comparison is against the best cost as of
-        // the iteration's start: autonomous items read bestCost (the CU's
-        // lanes are one wave, whose LDS reads precede lane 7's write);
-        // cooperative items read bestCostSnap, refreshed in the solve phase.
-        if (myCu >= 0) {
-          CuState& st = s_st[myCu];
-          if (iter == 0 || st.live) {
-            const float prod = __fmul_rn(pa.lambda, (float)(st.rate + kRuiBits));
-            const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
-            better = cost < (coop ? st.bestCostSnap : st.bestCost);
-            if (better && local == 7) {
-              st.bestCost = cost;
-              st.bestSatd = st.satd;
-              st.bestHasS = !lastIter && st.live;  // its gradient sums follow in this iteration
-            }
-          }
-          if (local < 6 && better) st.best[local] = st.cur[local];
-        }
-      }
-      PH_MARK(kPhCost)
-      if (lastIter) {  // uniform; the results below are written by other lanes
-        phase_sync(coop);
-        break;
-      }
-
-      // =============== gradients + normal equations (affine.cl:477-752) ===============
-      {
-        int S[5] = {0, 0, 0, 0, 0};
-        if (reuse && live) {
-#pragma unroll
-          for (int k = 0; k < 5; k++) S[k] = s_bestS[k][sbIdx];
-        } else if (live && !(VAME_ABLATE & 2)) {
-          // the neighbours' edge rows, extended by the left / right lanes' copies
-          // the sub-blocks above / below, computed here (kept live across the
-          // passes, the index was spilled)
-          const uint2 tb = s_bot[max(sbIdx - sbCols, 0)], bt = s_top[min(sbIdx + sbCols, C::NSB - 1)];
-          X[0] = ext_row(tb, dpp32<0x138, 0xF>((int)tb.y), dpp32<0x130, 0xF>((int)tb.x));
-          X[5] = ext_row(bt, dpp32<0x138, 0xF>((int)bt.y), dpp32<0x130, 0xF>((int)bt.x));
-          Geo gg = g;
-          int sxg = sx, syg = sy;
-          grad_sb(sxg, syg, gg, X, Og, S);
-          if (kDup & 2) {
-            int S2[5];
-            int sxd = sxg;
-            opaque(sxd);
-            grad_sb(sxd, syg, gg, X, Og, S2);
-            asm volatile("" ::"v"(S2[0] ^ S2[1] ^ S2[2] ^ S2[3] ^ S2[4]));
-          }
-          if (keepS && better) {  // the best iteration's sums, for the 3-CP seed reuse
-#pragma unroll
-            for (int k = 0; k < 5; k++) s_bestS[k][sbIdx] = S[k];
-          }
-        }
-        if (!(VAME_ABLATE & 4)) {
-          long long* dst = s_val[myCu < 0 ? 0 : myCu];
-          if (ncp == 2)
-            reduce_equations<2>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
-          else
-            reduce_equations<3>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
-          if constexpr ((kDup & 4) != 0) {
-            int ud = sx + 2;
-            opaque(ud);
-            if (ncp == 2)
-              reduce_equations<2>(S, ud, sy + 2, logS, myCu >= 0, coop, s_dup);
+          for (int r = 0; r < 4; r++)
+            X[r + 1] = ext_row(Pr[r], dpp32<0x138, 0xF>((int)Pr[r].y), dpp32<0x130, 0xF>((int)Pr[r].x));
+          s_top[sbIdx] = Pr[0];
+          s_bot[sbIdx] = Pr[3];
+          const int v = logS == 4 ? seg_sum_c<4>(satdLane)
+                        : logS == 5 ? seg_sum_c<5>(satdLane) : seg_sum_c<6>(satdLane);
+          if (leader) {
+            if (coop)
+              atomicAdd(&s_st[myCu].satd, v);
             else
-              reduce_equations<3>(S, ud, sy + 2, logS, myCu >= 0, coop, s_dup);
+              s_st[myCu].satd = v;
           }
         }
-      }
-      phase_sync(coop);
-      PH_MARK(kPhGradient)
+        phase_sync(coop);
+        PH_MARK(kPhPredict)
 
-      // =============== solve + CPMV update (affine.cl:782-893), per CU segment ===============
-      __builtin_amdgcn_s_setprio(kSolvePrio);
-      if (!(VAME_ABLATE & 1)) {
-        // the CU's lanes in its first wave solve it together
-        int cuS = myCu, loc = local;
-        opaque(cuS);  // recomputed, not loop-carried (VGPRs)
-        opaque(loc);
-        const bool solver = cuS >= 0 && loc < 64;
-        const bool act = solver && s_st[cuS].live;
-        const int Ls = 1 << logS;
-        double dd[6] = {0, 0, 0, 0, 0, 0};
-        long long* V = s_val[cuS < 0 ? 0 : cuS];
-        double* M = s_mat[cuS < 0 ? 0 : cuS];
-        const CuSlot cs = s_cu[cuS < 0 ? 0 : cuS];
-        if constexpr ((kDup & 16) != 0) {  // timing-only: a throw-away solve first
-          // on M itself, keeping V: the real solve below rebuilds M from V (no
-          // extra LDS, so the occupancy is the product build's)
-          double dd2[6] = {0, 0, 0, 0, 0, 0};
-          double* M2 = M;
+        // =============== cost, best update (affine.cl:416-457) ===============
+        // The cost is the SATD sum plus floor(lambda * (bits + 2)), the rate
+        // bits of the current CPMVs (calc_affine_bits, aux_functions.cl:2140-
+        // 2189) kept in CuState by the update step; the strict best is kept.
+        const bool lastIter = iter == niter;
+        bool better = false;  // keepS: this lane's CU improved
+        if constexpr (!keepS) {
+          // the CU's lane 7 prices and keeps the best; lanes 0-5 copy the CPMVs
+          int bet = 0;
+          if (myCu >= 0 && local == 7) {
+            CuState& st = s_st[myCu];
+            if (iter == 0 || st.live) {
+              const float prod = __fmul_rn(pa.lambda, (float)(st.rate + kRuiBits));
+              const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
+              if (cost < st.bestCost) {
+                st.bestCost = cost;
+                bet = 1;
+              }
+            }
+            st.satd = 0;
+          }
+          bet = __builtin_amdgcn_update_dpp(0, bet, 0x157, 0xF, 0xF, false);  // row_newbcast:7
+          if (myCu >= 0 && local < 6 && bet) s_st[myCu].best[local] = s_st[myCu].cur[local];
+        } else {
+          // 2-CP pass followed by a 3-CP pass: every lane of the CU prices it, so
+          // each knows whether its CU improved and keeps its gradient sums for
+          // the 3-CP seed reuse.  The comparison is against the best cost as of
+          // the iteration's start: autonomous items read bestCost (the CU's
+          // lanes are one wave, whose LDS reads precede lane 7's write);
+          // cooperative items read bestCostSnap, refreshed in the solve phase.
+          if (myCu >= 0) {
+            CuState& st = s_st[myCu];
+            if (iter == 0 || st.live) {
+              const float prod = __fmul_rn(pa.lambda, (float)(st.rate + kRuiBits));
+              const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
+              better = cost < (coop ? st.bestCostSnap : st.bestCost);
+              if (better && local == 7) {
+                st.bestCost = cost;
+                st.bestSatd = st.satd;
+                st.bestHasS = !lastIter && st.live;  // its gradient sums follow in this iteration
+              }
+            }
+            if (local < 6 && better) st.best[local] = st.cur[local];
+          }
+        }
+        PH_MARK(kPhCost)
+        if (lastIter) {  // uniform; the results below are written by other lanes
+          phase_sync(coop);
+          break;
+        }
+
+        // =============== gradients + normal equations (affine.cl:477-752) ===============
+        {
+          int S[5] = {0, 0, 0, 0, 0};
+          if (reuse && live) {
+#pragma unroll
+            for (int k = 0; k < 5; k++) S[k] = s_bestS[k][sbIdx];
+          } else if (live && !(VAME_ABLATE & 2)) {
+            // the neighbours' edge rows, extended by the left / right lanes' copies
+            // the sub-blocks above / below, computed here (kept live across the
+            // passes, the index was spilled)
+            const uint2 tb = s_bot[max(sbIdx - sbCols, 0)], bt = s_top[min(sbIdx + sbCols, C::NSB - 1)];
+            X[0] = ext_row(tb, dpp32<0x138, 0xF>((int)tb.y), dpp32<0x130, 0xF>((int)tb.x));
+            X[5] = ext_row(bt, dpp32<0x138, 0xF>((int)bt.y), dpp32<0x130, 0xF>((int)bt.x));
+            Geo gg = g;
+            int sxg = sx, syg = sy;
+            grad_sb(sxg, syg, gg, X, Og, S);
+            if (kDup & 2) {
+              int S2[5];
+              int sxd = sxg;
+              opaque(sxd);
+              grad_sb(sxd, syg, gg, X, Og, S2);
+              asm volatile("" ::"v"(S2[0] ^ S2[1] ^ S2[2] ^ S2[3] ^ S2[4]));
+            }
+            if (keepS && better) {  // the best iteration's sums, for the 3-CP seed reuse
+#pragma unroll
+              for (int k = 0; k < 5; k++) s_bestS[k][sbIdx] = S[k];
+            }
+          }
+          if (!(VAME_ABLATE & 4)) {
+            long long* dst = s_val[myCu < 0 ? 0 : myCu];
+            if (ncp == 2)
+              reduce_equations<2>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
+            else
+              reduce_equations<3>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
+            if constexpr ((kDup & 4) != 0) {
+              int ud = sx + 2;
+              opaque(ud);
+              if (ncp == 2)
+                reduce_equations<2>(S, ud, sy + 2, logS, myCu >= 0, coop, s_dup);
+              else
+                reduce_equations<3>(S, ud, sy + 2, logS, myCu >= 0, coop, s_dup);
+            }
+          }
+        }
+        phase_sync(coop);
+        PH_MARK(kPhGradient)
+
+        // =============== solve + CPMV update (affine.cl:782-893), per CU segment ===============
+        __builtin_amdgcn_s_setprio(kSolvePrio);
+        if (!(VAME_ABLATE & 1)) {
+          // the CU's lanes in its first wave solve it together
+          int cuS = myCu, loc = local;
+          opaque(cuS);  // recomputed, not loop-carried (VGPRs)
+          opaque(loc);
+          const bool solver = cuS >= 0 && loc < 64;
+          const bool act = solver && s_st[cuS].live;
+          const int Ls = 1 << logS;
+          double dd[6] = {0, 0, 0, 0, 0, 0};
+          long long* V = s_val[cuS < 0 ? 0 : cuS];
+          double* M = s_mat[cuS < 0 ? 0 : cuS];
+          const CuSlot cs = s_cu[cuS < 0 ? 0 : cuS];
+          if constexpr ((kDup & 16) != 0) {  // timing-only: a throw-away solve first
+            // on M itself, keeping V: the real solve below rebuilds M from V (no
+            // extra LDS, so the occupancy is the product build's)
+            double dd2[6] = {0, 0, 0, 0, 0, 0};
+            double* M2 = M;
+            if (ncp == 3)
+              seg_solve<3, true>(V, M2, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd2);
+            else
+              seg_solve<2, true>(V, M2, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd2);
+            asm volatile("" ::"v"(dd2[0]), "v"(dd2[1]), "v"(dd2[3]));
+            wave_sync();
+          }
           if (ncp == 3)
-            seg_solve<3, true>(V, M2, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd2);
+            seg_solve<3>(V, M, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd);
           else
-            seg_solve<2, true>(V, M2, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd2);
-          asm volatile("" ::"v"(dd2[0]), "v"(dd2[1]), "v"(dd2[3]));
-          wave_sync();
+            seg_solve<2>(V, M, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd);
+          // affine.cl:860-893, one CPMV component per lane: lane j < 6 of the
+          // CU applies scaleDeltaMvs to its delta (LT=(d0,d2), RT=(d1,d3),
+          // LB=(d4,d5)), clampCpmvs and clipCpmvs, and the CU's lane 7 sums
+          // the moved / cycle flags (DPP) into the CU's `live`
+          if (keepS && coop && solver && loc == 7) {  // the next cost phase's view; fresh SATD sums
+            CuState& st = s_st[cuS];
+            st.bestCostSnap = st.bestCost;
+            st.satd = 0;
+          }
+          bool liveNew = false;
+          if (act && loc < 8) {
+            CuState& st = s_st[cuS];
+            int f = 0, q = 0;
+            if (loc < 2 * ncp) {  // 2 CP: LB stays (0, 0)
+              const int j = loc;
+              const double d = M[j == 1 ? 2 : j == 2 ? 1 : j];
+              const int cj = st.cur[j], pj = st.prev[j];
+              int v = (int)((unsigned)cj + (unsigned)scale_delta(d));
+              v = clampi(v, kMvMin, kMvMax);
+              const int pos = (j & 1) ? ctuY + cs.y : ctuX + cs.x, lim = (j & 1) ? H : W;
+              v = clampi(v, shl(-128 - 8 - pos + 1, 4), shl(lim + 8 - pos - 1, 4));  // clipMv
+              f = (v != cj ? 1 : 0) | (v != pj ? 16 : 0);
+              st.prev[j] = cj;
+              st.cur[j] = v;
+              q = to_quarter(v);
+            }
+            // the rate of the new CPMVs (calc_affine_bits, aux_functions.cl:2140-2189)
+            // rides on the same lane sum: component j codes q_j - q_(j & 1) for
+            // j >= 2 (RT - LT from lane j - 2, LB - LT from lane j - 4)
+            {
+              const int q2 = dpp32<0x112, 0xF>(q), q4 = dpp32<0x114, 0xF>(q);
+              if (loc < 2 * ncp) f += eg_bits(q - (loc >= 4 ? q4 : loc >= 2 ? q2 : 0)) << 8;
+            }
+            f += dpp32<0x111, 0xF>(f);  // row_shr:1, 2, 4: lane 7 sums lanes 0..7
+            f += dpp32<0x112, 0xF>(f);
+            f += dpp32<0x114, 0xF>(f);
+            if (loc == 7) {
+              // moved, and not back to the previous (flag fields: bits 0-3 and 4-7)
+              liveNew = (f & 15) != 0 && ((f >> 4) & 15) != 0;
+              st.live = liveNew;
+              st.rate = f >> 8;
+            }
+          }
+          if (!coop) {  // leave once every CU of this wave is settled (wave-local)
+            if (__ballot(liveNew) == 0) {
+              __builtin_amdgcn_s_setprio(0);
+              break;
+            }
+          }
         }
-        if (ncp == 3)
-          seg_solve<3>(V, M, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd);
-        else
-          seg_solve<2>(V, M, s_eqmap, loc, Ls, act, coop, cs.lw, cs.lh, dd);
-        // affine.cl:860-893, one CPMV component per lane: lane j < 6 of the
-        // CU applies scaleDeltaMvs to its delta (LT=(d0,d2), RT=(d1,d3),
-        // LB=(d4,d5)), clampCpmvs and clipCpmvs, and the CU's lane 7 sums
-        // the moved / cycle flags (DPP) into the CU's `live`
-        if (keepS && coop && solver && loc == 7) {  // the next cost phase's view; fresh SATD sums
-          CuState& st = s_st[cuS];
-          st.bestCostSnap = st.bestCost;
-          st.satd = 0;
-        }
-        bool liveNew = false;
-        if (act && loc < 8) {
-          CuState& st = s_st[cuS];
-          int f = 0, q = 0;
-          if (loc < 2 * ncp) {  // 2 CP: LB stays (0, 0)
-            const int j = loc;
-            const double d = M[j == 1 ? 2 : j == 2 ? 1 : j];
-            const int cj = st.cur[j], pj = st.prev[j];
-            int v = (int)((unsigned)cj + (unsigned)scale_delta(d));
-            v = clampi(v, kMvMin, kMvMax);
-            const int pos = (j & 1) ? ctuY + cs.y : ctuX + cs.x, lim = (j & 1) ? H : W;
-            v = clampi(v, shl(-128 - 8 - pos + 1, 4), shl(lim + 8 - pos - 1, 4));  // clipMv
-            f = (v != cj ? 1 : 0) | (v != pj ? 16 : 0);
-            st.prev[j] = cj;
-            st.cur[j] = v;
-            q = to_quarter(v);
-          }
-          // the rate of the new CPMVs (calc_affine_bits, aux_functions.cl:2140-2189)
-          // rides on the same lane sum: component j codes q_j - q_(j & 1) for
-          // j >= 2 (RT - LT from lane j - 2, LB - LT from lane j - 4)
-          {
-            const int q2 = dpp32<0x112, 0xF>(q), q4 = dpp32<0x114, 0xF>(q);
-            if (loc < 2 * ncp) f += eg_bits(q - (loc >= 4 ? q4 : loc >= 2 ? q2 : 0)) << 8;
-          }
-          f += dpp32<0x111, 0xF>(f);  // row_shr:1, 2, 4: lane 7 sums lanes 0..7
-          f += dpp32<0x112, 0xF>(f);
-          f += dpp32<0x114, 0xF>(f);
-          if (loc == 7) {
-            // moved, and not back to the previous (flag fields: bits 0-3 and 4-7)
-            liveNew = (f & 15) != 0 && ((f >> 4) & 15) != 0;
-            st.live = liveNew;
-            st.rate = f >> 8;
-          }
-        }
-        if (!coop) {  // leave once every CU of this wave is settled (wave-local)
-          if (__ballot(liveNew) == 0) {
-            __builtin_amdgcn_s_setprio(0);
-            break;
-          }
+        __builtin_amdgcn_s_setprio(0);
+        phase_sync(coop);
+        PH_MARK(kPhSolve)
+        if (coop) {  // leave once every CU of the item is settled (flags read after the sync)
+          bool anyLive = false;
+          for (int k = cuB; k < cuE; k++) anyLive |= s_st[k].live != 0;
+          if (!anyLive) break;
         }
       }
-      __builtin_amdgcn_s_setprio(0);
+      // =============== results (affine.cl:928-957) ===============
+      if (lane < nCuW) {
+        int k = __lane_id();  // == lane, recomputed: not a spilled loop-carried copy
+        opaque(k);
+        k += cuB;
+        const CuState& st = s_st[k];
+        const CuSlot cs = s_cu[k];
+        const int mode = cs.align * 2 + (ncp - 2);
+        const size_t idx = (size_t)ctu * (cs.align ? kHalfCusPerCtu : kFullCusPerCtu) + cs.outOff;
+        pa.cost[mode][idx] = st.bestCost;
+        vame_cpmvs_dev o;
+        o.ncps = ncp;
+        o.ltx = st.best[0]; o.lty = st.best[1]; o.rtx = st.best[2];
+        o.rty = st.best[3]; o.lbx = st.best[4]; o.lby = st.best[5];
+        pa.cpmv[mode][idx] = o;
+      }
       phase_sync(coop);
-      PH_MARK(kPhSolve)
-      if (coop) {  // leave once every CU of the item is settled (flags read after the sync)
-        bool anyLive = false;
-        for (int k = cuB; k < cuE; k++) anyLive |= s_st[k].live != 0;
-        if (!anyLive) break;
+      PH_MARK(kPhTail)
+    };
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using T = std::true_type;
+    using F = std::false_type;
+    // keepS: the 2-CP pass feeds a 3-CP pass (seed reuse)
+    using KeepS = std::integral_constant<bool, run3>;
+    if (coop) {
+      if constexpr (run2) run_pass(I2{}, T{}, KeepS{});
+      if constexpr (run3) run_pass(I3{}, T{}, F{});
+    } else {
+      if constexpr (run2) run_pass(I2{}, F{}, KeepS{});
+      if constexpr (run2 && run3 && (VAME_DUP & 128) != 0) {  // timing-only: a barrier between the passes
+        __syncthreads();
       }
+      if constexpr (run3) run_pass(I3{}, F{}, F{});
     }
-    // =============== results (affine.cl:928-957) ===============
-    if (lane < nCuW) {
-      int k = __lane_id();  // == lane, recomputed: not a spilled loop-carried copy
-      opaque(k);
-      k += cuB;
-      const CuState& st = s_st[k];
-      const CuSlot cs = s_cu[k];
-      const int mode = cs.align * 2 + (ncp - 2);
-      const size_t idx = (size_t)ctu * (cs.align ? kHalfCusPerCtu : kFullCusPerCtu) + cs.outOff;
-      pa.cost[mode][idx] = st.bestCost;
-      vame_cpmvs_dev o;
-      o.ncps = ncp;
-      o.ltx = st.best[0]; o.lty = st.best[1]; o.rtx = st.best[2];
-      o.rty = st.best[3]; o.lbx = st.best[4]; o.lby = st.best[5];
-      pa.cpmv[mode][idx] = o;
-    }
-    phase_sync(coop);
-    PH_MARK(kPhTail)
-  };
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  using T = std::true_type;
-  using F = std::false_type;
-  // keepS: the 2-CP pass feeds a 3-CP pass (seed reuse)
-  using KeepS = std::integral_constant<bool, run3>;
-  if (coop) {
-    if constexpr (run2) run_pass(I2{}, T{}, KeepS{});
-    if constexpr (run3) run_pass(I3{}, T{}, F{});
-  } else {
-    if constexpr (run2) run_pass(I2{}, F{}, KeepS{});
-    if constexpr (run2 && run3 && (VAME_DUP & 128) != 0) {  // timing-only: a barrier between the passes
+    if (!C::AUTO || task + tstep >= nTasks) break;
+    // the next task's CU slots into this task's (cooperative: after every wave's
+    // last read of them, autonomous: the wave's own, read by this wave only)
+    if (coop) {
+      if (tid < kTaskCu) s_cu[tid] = s_cu[min(task + 1, kMaxTasks - 1) * kTaskCu + tid];
       __syncthreads();
+    } else {
+      if (lane < kTaskCu) s_cu[wv * kTaskCu + lane] = s_cu[min(task + 4, kMaxTasks - 1) * kTaskCu + lane];
+      wave_sync();
     }
-    if constexpr (run3) run_pass(I3{}, F{}, F{});
   }
   PH_FLUSH
   PC_FLUSH
