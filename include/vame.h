@@ -125,8 +125,10 @@ int vame_get_timing(vame_ctx* ctx, int kernel_class, double* total_ms, int* laun
  * them; half128 != 0: the affine_me_half packing, 0: the CTU packing -- cover each of the CTU's
  * candidate CUs of `align`: hits[0 .. {201|284}) indexed by the output offset
  * RETURN_STRIDE[group] + cuIdx (affine.cl:936 / :1929).  A valid partition
- * covers every CU exactly once.  Also returns the item counts per kernel
- * class (quad, ctu, half) in items3 when non-NULL. */
+ * covers every CU exactly once (the quadrant items of one-alignment launches;
+ * VAME_E_INVALID if those of both-alignment launches cover differently).
+ * Also returns the item counts per kernel class (quad -- of a both-alignment
+ * launch --, ctu, half) in items3 when non-NULL. */
 int vame_template_coverage(int half128, int align, int32_t* hits, int32_t* items3);
 
 /* Geometry / host helpers (no device work). */

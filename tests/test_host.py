@@ -47,19 +47,25 @@ def test_version_and_errors():
     assert L.vame_cus_per_ctu(0) == 201 and L.vame_cus_per_ctu(1) == 284
 
 
-@pytest.mark.parametrize("tasks,chain,quad_items", [("8", "1", 36), ("8", "0", 44), ("4", "0", 72), ("1", "1", None)])
+@pytest.mark.parametrize("tasks,chain,mix,quad_items", [("16", "1", "1", 20), ("16", "1", "0", 24), ("8", "1", "1", 32),
+                                                      ("8", "0", "0", 44), ("4", "0", "0", 72), ("1", "1", "1", 228),
+                                                      ("16", "0", "1", 32)])
 @pytest.mark.parametrize("half128", [1, 0])
-def test_work_items_cover_every_cu_once(half128, tasks, chain, quad_items, monkeypatch):
+def test_work_items_cover_every_cu_once(half128, tasks, chain, mix, quad_items, monkeypatch):
     """The engine's work-item templates (vame_create's build_templates, run on
     the host without a device) partition the CTU's candidate CUs: every FULL
     (201) and HALF (284) output offset is covered by exactly one item's CU
     slot -- with the 128x64 / 64x128 CUs in 512-thread affine_me_half items
     (one CU each, the default) or packed two per 1024-thread CTU item, and
-    for every quadrant packing: autonomous items of 8 wave tasks (default),
-    4 or 1, the FULL 64x64 / 64x32 / 32x64 groups chained into one
-    cooperative item per quadrant (default) or one item each."""
+    for every quadrant packing: autonomous items of 16 wave tasks (default),
+    8, 4 or 1; the cooperative groups (FULL 64x64 / 64x32 / 32x64, HALF
+    64x32 + 32x64) chained into one item per quadrant (default) or one item
+    each; a launch of both alignments on items mixing them (default) or on
+    the two alignments' own items.  quad_items: the quadrant items per CTU of
+    a both-alignment launch."""
     monkeypatch.setenv("VAME_TASKS", tasks)
     monkeypatch.setenv("VAME_CHAIN", chain)
+    monkeypatch.setenv("VAME_MIX", mix)
     L = _lib.lib()
     items = (ctypes.c_int32 * 3)()
     for align, n in ((0, 201), (1, 284)):

@@ -20,7 +20,6 @@ using namespace vame;
 
 static_assert(sizeof(vame_cpmvs) == 28, "Cpmvs layout (typedef.h)");
 static_assert(sizeof(vame_cpmvs_dev) == 28, "Cpmvs layout (typedef.h)");
-static_assert(sizeof(CuSlot) == 16, "CuSlot layout");
 
 static thread_local char g_hip_err[256] = "";
 
@@ -44,7 +43,7 @@ struct vame_ctx {
   Item* dBig3 = nullptr;
   Item* dBig1 = nullptr;
   Item* dHalf = nullptr;
-  int nQuadFull = 0, nQuadHalf = 0, nBig3 = 0, nBig1 = 0, nHalf = 0;
+  int nQuadFull = 0, nQuadHalf = 0, nQuadBoth = 0, nBig3 = 0, nBig1 = 0, nHalf = 0;
   // which packing a launch uses (VAME_HALF128): 0 always dBig3, 1 always
   // dBig1 + dHalf, 2 (default) dBig1 + dHalf for launches of at least
   // halfMinPairs (POC, refIdx) pairs (VAME_HALF_MIN_PAIRS, default 16), dBig3
@@ -111,8 +110,8 @@ void set_slot(CuSlot& s, const CuDesc& c, int sbBase) {
   s.lw = (uint8_t)ilog2(c.w);
   s.lh = (uint8_t)ilog2(c.h);
   s.align = (uint8_t)c.align;
-  s.outOff = (int16_t)c.outOff;
-  s.sbBase = (int16_t)sbBase;
+  s.outOff = (uint16_t)c.outOff;
+  s.sbBase = (uint16_t)sbBase;
 }
 
 // Cooperative item: tasks of CUs of one size, each CU spanning nsb >= 64
@@ -136,7 +135,8 @@ Item make_coop_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& task
       if (nsb_of(c) != nsb) abort();
     if (nsb < 64 || n * nsb > threads || n > stride) abort();
     for (int i = 0; i < n; i++) set_slot(it.cu[t * stride + i], tasks[t][i], i * nsb);
-    it.cu[t * stride].task = n | (ilog2(nsb) << 8);
+    it.cu[t * stride].taskCus = (uint8_t)n;
+    it.cu[t * stride].taskLogL = (uint16_t)ilog2(nsb);
     it.nCu = (int16_t)(t * stride + n);
   }
   return it;
@@ -167,7 +167,8 @@ Item make_auto_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& task
       if (nsb_of(c) != nsb) abort();
     if (n * nsb > 64 || nsb < 16 || n > kTaskCu) abort();  // the kernel's segment sums handle 16 / 32 / 64
     for (int i = 0; i < n; i++) set_slot(it.cu[t * kTaskCu + i], tasks[t][i], (int)(t % 4) * 64 + i * nsb);
-    it.cu[t * kTaskCu].task = n | (ilog2(nsb) << 8);
+    it.cu[t * kTaskCu].taskCus = (uint8_t)n;
+    it.cu[t * kTaskCu].taskLogL = (uint16_t)ilog2(nsb);
   }
   return it;
 }
@@ -202,8 +203,13 @@ void pack_autonomous(int qx, int qy, std::vector<CuDesc> cus, std::vector<Item>&
 //              items of `tasks` wave tasks
 //   quadHalf : HALF groups per quadrant (no HALF CU crosses a quadrant):
 //              64x32 + 32x64 cooperative, the rest autonomous
+//   quadBoth : the items of a launch of both alignments: with `mixed`, per
+//              quadrant one cooperative chain of the FULL and HALF tasks and
+//              autonomous items over both alignments' CUs; else quadFull +
+//              quadHalf
 void build_templates(std::vector<Item>& big, std::vector<Item>& halfItems, std::vector<Item>& quadFull,
-                     std::vector<Item>& quadHalf, bool half, int tasks, bool chainCoop) {
+                     std::vector<Item>& quadHalf, std::vector<Item>& quadBoth, bool half, int tasks,
+                     bool chainCoop, bool mixed) {
   for (int g = 0; g < kFullGroups; g++) {
     const int w = kFullW[g], h = kFullH[g], n = (kCtu * kCtu) / (w * h), cols = kCtu / w;
     if (w == 128 || h == 128) {
@@ -222,11 +228,12 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& halfItems, std::
       }
     }
   }
+  std::vector<Item> bothCoop, bothAuto;
   for (int q = 0; q < 4; q++) {
     const int qx = (q & 1) * 64, qy = (q >> 1) * 64;
     auto inq = [&](int x, int y) { return x >= qx && x < qx + 64 && y >= qy && y < qy + 64; };
-    std::vector<CuDesc> small;
-    std::vector<std::vector<CuDesc>> chain;
+    std::vector<CuDesc> fullSmall, halfSmall, halfBig;
+    std::vector<std::vector<CuDesc>> fullCoop;  // a task per group
     for (int g = 0; g < kFullGroups; g++) {
       const int w = kFullW[g], h = kFullH[g], n = (kCtu * kCtu) / (w * h), cols = kCtu / w;
       if (w == 128 || h == 128) continue;
@@ -236,26 +243,44 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& halfItems, std::
         if (inq(x, y)) c.push_back({x, y, w, h, 0, kFullStride[g] + k});
       }
       if (w * h / 16 <= 64)
-        small.insert(small.end(), c.begin(), c.end());
-      else if (chainCoop)
-        chain.push_back(c);
+        fullSmall.insert(fullSmall.end(), c.begin(), c.end());
       else
-        quadFull.push_back(make_coop_item(qx, qy, c, Cfg<kKindQuad>::THREADS));
+        fullCoop.push_back(c);
     }
-    if (!chain.empty()) quadFull.push_back(make_coop_item(qx, qy, chain, Cfg<kKindQuad>::THREADS));
-    pack_autonomous(qx, qy, small, quadFull, tasks);
-    std::vector<CuDesc> bigHalf;
-    small.clear();
     for (int g = 0; g < kHalfGroups; g++)
       for (int k = 0; k < kHalfN[g]; k++) {
         const int x = kHalfX8[g][k] * 8, y = kHalfY8[g][k] * 8;
         if (!inq(x, y)) continue;
         if (x + kHalfW[g] > qx + 64 || y + kHalfH[g] > qy + 64) abort();
         const CuDesc c{x, y, kHalfW[g], kHalfH[g], 1, kHalfStride[g] + k};
-        (nsb_of(c) > 64 ? bigHalf : small).push_back(c);
+        (nsb_of(c) > 64 ? halfBig : halfSmall).push_back(c);
       }
-    if (!bigHalf.empty()) quadHalf.push_back(make_coop_item(qx, qy, bigHalf, Cfg<kKindQuad>::THREADS));
-    pack_autonomous(qx, qy, small, quadHalf, tasks);
+    // cooperative tasks: one chained item, or an item per task
+    auto coop = [&](const std::vector<std::vector<CuDesc>>& t, std::vector<Item>& out) {
+      if (chainCoop)
+        out.push_back(make_coop_item(qx, qy, t, Cfg<kKindQuad>::THREADS));
+      else
+        for (auto& cus : t) out.push_back(make_coop_item(qx, qy, cus, Cfg<kKindQuad>::THREADS));
+    };
+    coop(fullCoop, quadFull);
+    pack_autonomous(qx, qy, fullSmall, quadFull, tasks);
+    if (!halfBig.empty()) quadHalf.push_back(make_coop_item(qx, qy, halfBig, Cfg<kKindQuad>::THREADS));
+    pack_autonomous(qx, qy, halfSmall, quadHalf, tasks);
+    if (mixed) {  // both alignments in one item set: every quadrant's cooperative chain first
+      std::vector<std::vector<CuDesc>> t(fullCoop);
+      if (!halfBig.empty()) t.push_back(halfBig);
+      coop(t, bothCoop);
+      std::vector<CuDesc> small(fullSmall);
+      small.insert(small.end(), halfSmall.begin(), halfSmall.end());
+      pack_autonomous(qx, qy, small, bothAuto, tasks);
+    }
+  }
+  if (mixed) {
+    quadBoth = bothCoop;
+    quadBoth.insert(quadBoth.end(), bothAuto.begin(), bothAuto.end());
+  } else {
+    quadBoth = quadFull;
+    quadBoth.insert(quadBoth.end(), quadHalf.begin(), quadHalf.end());
   }
 }
 
@@ -381,10 +406,13 @@ int env_int(const char* name, int dflt) {
   return e && *e ? atoi(e) : dflt;
 }
 
-// wave tasks per autonomous quadrant item (VAME_TASKS, 1..8)
-int tasks_per_item() { return std::min(kMaxTasks, std::max(1, env_int("VAME_TASKS", 8))); }
+// wave tasks per autonomous quadrant item (VAME_TASKS, 1..16)
+int tasks_per_item() { return std::min(kMaxTasks, std::max(1, env_int("VAME_TASKS", 16))); }
+static_assert(kFullCusPerCtu <= 512 && kHalfCusPerCtu <= 512, "CuSlot::outOff");
 // one cooperative item per quadrant for the FULL 64x64 / 64x32 / 32x64 groups (VAME_CHAIN)
 bool chain_coop() { return env_int("VAME_CHAIN", 1) != 0; }
+// launches of both alignments use items mixing them (VAME_MIX)
+bool mix_aligns() { return env_int("VAME_MIX", 1) != 0; }
 
 // The kernel instance of a launch mode (vame_kernel.h MODE: 1 = 2-CP only,
 // 2 = 3-CP only, 3 = 2-CP then 3-CP).
@@ -471,8 +499,13 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
   };
   auto quad = [&](const KParams& kp) -> int {
     KParams kq = kp;
-    kq.items = quadFull ? c->dQuad : c->dQuad + c->nQuadFull;
-    kq.nItems = (quadFull ? c->nQuadFull : 0) + (quadHalf ? c->nQuadHalf : 0);
+    if (quadFull && quadHalf) {
+      kq.items = c->dQuad + c->nQuadFull + c->nQuadHalf;
+      kq.nItems = c->nQuadBoth;
+    } else {
+      kq.items = quadFull ? c->dQuad : c->dQuad + c->nQuadFull;
+      kq.nItems = quadFull ? c->nQuadFull : c->nQuadHalf;
+    }
     const unsigned grid = block_grid(c, 0, kq);
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 0, t0, t1));
@@ -600,12 +633,13 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (device < 0 || device >= ndev) return VAME_E_INVALID;
   DeviceGuard guard(device);
   VAME_HIP(guard.err);
-  std::vector<Item> big3, big1, hf, qf, qh, unused;
+  std::vector<Item> big3, big1, hf, qf, qh, qb, unused;
   const int tasks = tasks_per_item();
-  build_templates(big3, unused, qf, qh, false, tasks, chain_coop());
+  build_templates(big3, unused, qf, qh, qb, false, tasks, chain_coop(), mix_aligns());
   qf.clear();
   qh.clear();
-  build_templates(big1, hf, qf, qh, true, tasks, chain_coop());
+  qb.clear();
+  build_templates(big1, hf, qf, qh, qb, true, tasks, chain_coop(), mix_aligns());
   vame_ctx* c = new vame_ctx();
   c->device = device;
   c->W = width;
@@ -619,8 +653,10 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   c->halfMinPairs = std::max(1, env_int("VAME_HALF_MIN_PAIRS", 16));
   c->nQuadFull = (int)qf.size();
   c->nQuadHalf = (int)qh.size();
-  std::vector<Item> quad(qf);
+  c->nQuadBoth = (int)qb.size();
+  std::vector<Item> quad(qf);  // [FULL][HALF][both alignments]
   quad.insert(quad.end(), qh.begin(), qh.end());
+  quad.insert(quad.end(), qb.begin(), qb.end());
   hipError_t e = hipMalloc(&c->dQuad, quad.size() * sizeof(Item));
   // tuning knobs of the block order (defaults measured on MI355X)
   const int xcdOrder = env_int("VAME_XCD_ORDER", 0);
@@ -707,20 +743,28 @@ int vame_affine_me(vame_ctx* c, const uint16_t* ref, const uint16_t* cur, float 
 
 int vame_template_coverage(int half128, int align, int32_t* hits, int32_t* items3) {
   if (!hits || (align != 0 && align != 1)) return VAME_E_INVALID;
-  std::vector<Item> big, hf, qf, qh;
-  build_templates(big, hf, qf, qh, half128 != 0, tasks_per_item(), chain_coop());
+  std::vector<Item> big, hf, qf, qh, qb;
+  build_templates(big, hf, qf, qh, qb, half128 != 0, tasks_per_item(), chain_coop(), mix_aligns());
   const int n = align ? kHalfCusPerCtu : kFullCusPerCtu;
+  // the one-alignment item set and the both-alignment one must cover alike
+  std::vector<int32_t> both(n, 0);
   for (int i = 0; i < n; i++) hits[i] = 0;
-  for (const auto* v : {&big, &hf, &qf, &qh})
+  for (const auto* v : {&big, &hf, &qf, &qh, &qb})
     for (const Item& it : *v)
       for (int k = 0; k < it.nCu; k++) {
         const CuSlot& s = it.cu[k];
         if (s.lw == 0 || s.align != align) continue;  // lw 0: an unused slot
-        if (s.outOff < 0 || s.outOff >= n) return VAME_E_INVALID;
-        hits[s.outOff]++;
+        if (s.outOff >= n) return VAME_E_INVALID;
+        (v == &qb ? both[s.outOff] : hits[s.outOff])++;
       }
+  for (const auto* v : {&big, &hf})
+    for (const Item& it : *v)
+      for (int k = 0; k < it.nCu; k++)
+        if (it.cu[k].lw != 0 && it.cu[k].align == align) both[it.cu[k].outOff]++;
+  for (int i = 0; i < n; i++)
+    if (both[i] != hits[i]) return VAME_E_INVALID;
   if (items3) {
-    items3[0] = (int32_t)(qf.size() + qh.size());
+    items3[0] = (int32_t)qb.size();
     items3[1] = (int32_t)big.size();
     items3[2] = (int32_t)hf.size();
   }

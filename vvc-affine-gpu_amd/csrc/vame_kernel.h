@@ -39,7 +39,7 @@
 namespace vame {
 
 constexpr int kMaxCu = 16;    // CU state slots per workgroup (LDS)
-constexpr int kMaxTasks = 8;  // autonomous items: wave tasks (wave w runs tasks w, w + 4)
+constexpr int kMaxTasks = 16;  // autonomous items: wave tasks (wave w runs tasks w, w + 4, ...)
 constexpr int kTaskCu = 4;    // CUs per wave task (<= 64 sub-blocks, >= 16 each)
 constexpr int kItemCu = kMaxTasks * kTaskCu;  // CU slots per work item
 constexpr int kThreads = 256;  // quadrant workgroups
@@ -51,15 +51,16 @@ struct vame_cpmvs_dev {
   int32_t ncps, ltx, lty, rtx, rty, lbx, lby;
 };
 
-struct CuSlot {     // 16 bytes
-  int16_t x, y;     // CTU-relative position
-  uint8_t lw, lh;   // log2 width / height
-  uint8_t align;    // 0 FULL, 1 HALF
-  uint8_t pad0;
-  int16_t outOff;   // RETURN_STRIDE[group] + cuIdx
-  int16_t sbBase;   // first sub-block of this CU inside the workgroup (prediction rows)
-  int32_t task;     // a task's first slot: CUs in the task | log2 lanes per CU << 8
+struct CuSlot {          // 8 bytes
+  uint8_t x, y;          // CTU-relative position
+  uint8_t lw : 4, lh : 4;  // log2 width / height
+  uint8_t align : 1;     // 0 FULL, 1 HALF
+  uint8_t taskCus : 5;   // a task's first slot: CUs in the task (0 elsewhere)
+  uint16_t outOff : 9;   // RETURN_STRIDE[group] + cuIdx
+  uint16_t taskLogL : 4;  // a task's first slot: log2 lanes per CU
+  uint16_t sbBase;       // first sub-block of this CU inside the workgroup (prediction rows)
 };
+static_assert(sizeof(CuSlot) == 8, "CuSlot packing");
 
 // An item's CUs come in tasks of one CU size each, run over the item's one
 // staged tile: a cooperative item's tasks one after another by the whole
@@ -1606,10 +1607,10 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   for (int task = coop ? 0 : __builtin_amdgcn_readfirstlane(wv);; task += tstep) {
     // ---- CUs of this wave, this lane's CU and sub-blocks (fixed for the task)
     const int lidx = coop ? tid : lane;
-    const int ti = s_cu[coop ? 0 : wv * kTaskCu].task;
+    const CuSlot t0 = s_cu[coop ? 0 : wv * kTaskCu];
     int cuB = coop ? 0 : wv * kTaskCu;
-    int cuE = cuB + (ti & 0xFF);
-    int logL = (ti >> 8) & 0xFF;
+    int cuE = cuB + t0.taskCus;
+    int logL = t0.taskLogL;
     cuB = __builtin_amdgcn_readfirstlane(cuB);
     cuE = __builtin_amdgcn_readfirstlane(cuE);
     logL = __builtin_amdgcn_readfirstlane(logL);
