@@ -430,10 +430,11 @@ def test_property_translation_1080p(engines, d):
                                  {"VAME_GRAPH": "1"}, {"VAME_GRAPH": "1", "VAME_HALF128": "1"},
                                  {"VAME_GRAPH": "1", "VAME_STREAMS": "2"}, {"VAME_MIX": "0"},
                                  {"VAME_TASKS": "8"}, {"VAME_TASKS": "4", "VAME_CHAIN": "0", "VAME_MIX": "0"},
-                                 {"VAME_TASKS": "1"}],
+                                 {"VAME_TASKS": "1"}, {"VAME_CLAIM": "0"}],
                          ids=["half512_packing", "ctu1024_packing", "two_streams", "two_streams_half512",
                               "ctu_first", "graph", "graph_half512", "graph_two_streams", "aligns_unmixed",
-                              "items_of_8", "items_of_4_unchained_unmixed", "items_of_1_task"])
+                              "items_of_8", "items_of_4_unchained_unmixed", "items_of_1_task",
+                              "static_tasks"])
 def test_launch_structure_variants(env, monkeypatch):
     """The engine's launch-structure knobs (read at vame_create) change only
     where the work runs: VAME_HALF128=1 gives every 128x64 / 64x128 CU a
@@ -444,7 +445,8 @@ def test_launch_structure_variants(env, monkeypatch):
     stream (all but the first without the AQL barrier bit, the default);
     VAME_QUAD_FIRST=0 issues the 128-class kernels before the quadrant kernel;
     VAME_TASKS=8 / 4 / 1 packs 8 / 4 / 1 wave tasks per autonomous quadrant
-    item (default 16: each wave runs four over the one staged tile),
+    item (default 16 over the one staged tile, each wave claiming the next
+    task as it finishes; VAME_CLAIM=0: wave w runs tasks w, w + 4, ...),
     VAME_CHAIN=0 gives each cooperative group an item of its own instead of
     one chained cooperative item per quadrant, VAME_MIX=0 runs a launch of
     both alignments on the two alignments' own items; VAME_GRAPH=1 captures a call's launches

@@ -92,6 +92,22 @@ struct vame_ctx {
 
 namespace {
 
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+
+// wave tasks per autonomous quadrant item (VAME_TASKS, 1..16)
+int tasks_per_item() { return std::min(kMaxTasks, std::max(1, env_int("VAME_TASKS", 16))); }
+static_assert(kFullCusPerCtu <= 512 && kHalfCusPerCtu <= 512, "CuSlot::outOff");
+// one cooperative item per quadrant chaining its cooperative groups (VAME_CHAIN)
+bool chain_coop() { return env_int("VAME_CHAIN", 1) != 0; }
+// launches of both alignments use items mixing them (VAME_MIX)
+bool mix_aligns() { return env_int("VAME_MIX", 1) != 0; }
+// autonomous waves claim their next task from an LDS counter as they finish
+// (VAME_CLAIM=0: wave w runs tasks w, w + 4, ...)
+bool claim_tasks() { return env_int("VAME_CLAIM", 1) != 0; }
+
 int ilog2(int v) {
   int l = 0;
   while ((1 << (l + 1)) <= v) l++;
@@ -147,16 +163,17 @@ Item make_coop_item(int rx, int ry, const std::vector<CuDesc>& cus, int threads)
 
 // Autonomous item: up to kMaxTasks wave tasks, each CUs of ONE size (<= 64
 // sub-blocks, one lane per sub-block), so a task's segment size is uniform.
-// Wave w runs tasks w, w + 4, ... over the one staged tile: task t holds CU
+// Wave w runs task w, then (claim) the next unclaimed one as it finishes, or
+// tasks w + 4, w + 8, ..., over the one staged tile: task t holds CU
 // slots t * kTaskCu .. (its first slot carries the task's CU count and lanes
-// per CU) and the wave's prediction rows (t % 4) * 64 ...  Unused slots stay
-// zero (lw 0).
-Item make_auto_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& tasks) {
+// per CU) and the running wave's prediction rows.  Unused slots stay zero
+// (lw 0).
+Item make_auto_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& tasks, bool claim) {
   Item it;
   memset(&it, 0, sizeof(it));
   it.rx = (int16_t)rx;
   it.ry = (int16_t)ry;
-  it.coop = 0;
+  it.coop = claim ? 2 : 0;
   if (tasks.empty() || (int)tasks.size() > kMaxTasks) abort();
   it.nTasks = (int16_t)tasks.size();
   it.nCu = (int16_t)(tasks.size() * kTaskCu);
@@ -166,7 +183,7 @@ Item make_auto_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& task
     for (auto& c : tasks[t])
       if (nsb_of(c) != nsb) abort();
     if (n * nsb > 64 || nsb < 16 || n > kTaskCu) abort();  // the kernel's segment sums handle 16 / 32 / 64
-    for (int i = 0; i < n; i++) set_slot(it.cu[t * kTaskCu + i], tasks[t][i], (int)(t % 4) * 64 + i * nsb);
+    for (int i = 0; i < n; i++) set_slot(it.cu[t * kTaskCu + i], tasks[t][i], i * nsb);
     it.cu[t * kTaskCu].taskCus = (uint8_t)n;
     it.cu[t * kTaskCu].taskLogL = (uint16_t)ilog2(nsb);
   }
@@ -188,7 +205,7 @@ void pack_autonomous(int qx, int qy, std::vector<CuDesc> cus, std::vector<Item>&
   for (size_t w = 0; w < waves.size(); w += perItem) {
     std::vector<std::vector<CuDesc>> grp(waves.begin() + w,
                                          waves.begin() + std::min(waves.size(), w + perItem));
-    out.push_back(make_auto_item(qx, qy, grp));
+    out.push_back(make_auto_item(qx, qy, grp, claim_tasks()));
   }
 }
 
@@ -401,18 +418,7 @@ std::vector<int32_t> build_order(int nCtus, int cols, int groupCombos, int xcdOr
   return order;
 }
 
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e && *e ? atoi(e) : dflt;
-}
 
-// wave tasks per autonomous quadrant item (VAME_TASKS, 1..16)
-int tasks_per_item() { return std::min(kMaxTasks, std::max(1, env_int("VAME_TASKS", 16))); }
-static_assert(kFullCusPerCtu <= 512 && kHalfCusPerCtu <= 512, "CuSlot::outOff");
-// one cooperative item per quadrant for the FULL 64x64 / 64x32 / 32x64 groups (VAME_CHAIN)
-bool chain_coop() { return env_int("VAME_CHAIN", 1) != 0; }
-// launches of both alignments use items mixing them (VAME_MIX)
-bool mix_aligns() { return env_int("VAME_MIX", 1) != 0; }
 
 // The kernel instance of a launch mode (vame_kernel.h MODE: 1 = 2-CP only,
 // 2 = 3-CP only, 3 = 2-CP then 3-CP).

@@ -58,7 +58,7 @@ struct CuSlot {          // 8 bytes
   uint8_t taskCus : 5;   // a task's first slot: CUs in the task (0 elsewhere)
   uint16_t outOff : 9;   // RETURN_STRIDE[group] + cuIdx
   uint16_t taskLogL : 4;  // a task's first slot: log2 lanes per CU
-  uint16_t sbBase;       // first sub-block of this CU inside the workgroup (prediction rows)
+  uint16_t sbBase;       // first sub-block of this CU in its task (prediction rows; autonomous tasks: + 64 * wave)
 };
 static_assert(sizeof(CuSlot) == 8, "CuSlot packing");
 
@@ -70,7 +70,7 @@ static_assert(sizeof(CuSlot) == 8, "CuSlot packing");
 struct Item {
   int16_t nCu;      // CU slots (host view; unused slots have lw 0)
   int16_t rx, ry;   // region origin (CTU-relative)
-  int16_t coop;     // 1: cooperative (a task's CUs span waves)
+  int16_t coop;     // bit 0: cooperative (a task's CUs span waves); bit 1: autonomous waves claim tasks
   int16_t nTasks;
   int16_t rw, rh;   // affine_me_half items: the region's extent (the CU's); 0 elsewhere
   int16_t pad;
@@ -1485,7 +1485,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   __shared__ uint8_t s_eqmap[80];
   __shared__ CuState s_st[C::MAXCU];
   __shared__ CuSlot s_cu[C::ITEMCU];
-  __shared__ int s_hdr[4];
+  __shared__ int s_hdr[2];  // item header, next wave task to claim
   __shared__ long long s_dup[(VAME_DUP & 4) ? kNumMom : 1];
 
   const int tid = threadIdx.x;
@@ -1576,7 +1576,10 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   if (tid < C::ITEMCU) s_cu[tid] = it->cu[tid];
   if (tid < 48) s_coef[tid] = reinterpret_cast<const uint4*>(&kCoefTab)[tid];
   if (tid < 80) s_eqmap[tid] = kEqMap.v[tid];
-  if (tid == 0) s_hdr[0] = it->coop | (it->nTasks << 16);
+  if (tid == 0) {
+    s_hdr[0] = it->coop | (it->nTasks << 16);
+    s_hdr[1] = 4;  // tasks 0 .. 3: waves 0 .. 3
+  }
   for (int i = tid; i < C::MAXCU * kNumMom; i += C::THREADS) (&s_val[0][0])[i] = 0;
   PH_INIT
   if (!regionOut) {
@@ -1590,7 +1593,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   PH_START
   const int hdr = __builtin_amdgcn_readfirstlane(s_hdr[0]);
   const int nTasks = (hdr >> 16) & 0xFF;
-  const bool coop = !C::AUTO || (hdr & 0xFF) != 0;
+  const bool coop = !C::AUTO || (hdr & 1) != 0;
+  const bool claim = C::AUTO && (hdr & 2) != 0;  // autonomous: waves claim tasks as they finish
   PH_MARK(kPhStage)
   if (!coop && wv >= nTasks) {  // wave-uniform: an autonomous wave without CUs
     PH_FLUSH
@@ -1598,13 +1602,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   }
 
   // Tasks over the one staged tile: a cooperative item's tasks one after
-  // another, an autonomous wave's tasks wv, wv + 4, ...  Each task's CU slots
+  // another, an autonomous wave's tasks wv, wv + 4, ... (or, claiming, wv
+  // and then the next unclaimed task when it finishes).  Each task's CU slots
   // are first moved into slots 0 .. (cooperative) or the wave's own slots
   // wv * kTaskCu .. (autonomous: its CU state, moments and systems; its
   // sub-blocks use the wave's own prediction rows, so its tasks need no
   // workgroup barrier).
-  const int tstep = coop ? 1 : 4;
-  for (int task = coop ? 0 : __builtin_amdgcn_readfirstlane(wv);; task += tstep) {
+  for (int task = coop ? 0 : __builtin_amdgcn_readfirstlane(wv);;) {
     // ---- CUs of this wave, this lane's CU and sub-blocks (fixed for the task)
     const int lidx = coop ? tid : lane;
     const CuSlot t0 = s_cu[coop ? 0 : wv * kTaskCu];
@@ -1631,7 +1635,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       g.h = 1 << g.lh;
       g.x = ctuX + cs.x;
       g.y = ctuY + cs.y;
-      sbIdx = cs.sbBase + local;
+      sbIdx = (coop ? 0 : wv * 64) + cs.sbBase + local;  // autonomous: the running wave's rows
       sbCols = 1 << (g.lw - 2);
       sx = (local & (sbCols - 1)) << 2;
       sy = (local >> (g.lw - 2)) << 2;
@@ -2003,16 +2007,24 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       }
       if constexpr (run3) run_pass(I3{}, F{}, F{});
     }
-    if (!C::AUTO || task + tstep >= nTasks) break;
+    if (!C::AUTO) break;
     // the next task's CU slots into this task's (cooperative: after every wave's
     // last read of them, autonomous: the wave's own, read by this wave only)
+    int next = task + (coop ? 1 : 4);
+    if (claim) {
+      int v = 0;
+      if (lane == 0) v = atomicAdd(&s_hdr[1], 1);
+      next = __builtin_amdgcn_readfirstlane(v);
+    }
+    if (next >= nTasks) break;
     if (coop) {
-      if (tid < kTaskCu) s_cu[tid] = s_cu[min(task + 1, kMaxTasks - 1) * kTaskCu + tid];
+      if (tid < kTaskCu) s_cu[tid] = s_cu[min(next, kMaxTasks - 1) * kTaskCu + tid];
       __syncthreads();
     } else {
-      if (lane < kTaskCu) s_cu[wv * kTaskCu + lane] = s_cu[min(task + 4, kMaxTasks - 1) * kTaskCu + lane];
+      if (lane < kTaskCu) s_cu[wv * kTaskCu + lane] = s_cu[min(next, kMaxTasks - 1) * kTaskCu + lane];
       wave_sync();
     }
+    task = next;
   }
   PH_FLUSH
   PC_FLUSH
