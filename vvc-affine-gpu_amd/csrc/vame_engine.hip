@@ -120,14 +120,13 @@ struct CuDesc {
 
 int nsb_of(const CuDesc& c) { return c.w * c.h / 16; }
 
-void set_slot(CuSlot& s, const CuDesc& c, int sbBase) {
+void set_slot(CuSlot& s, const CuDesc& c) {
   s.x = (int16_t)c.x;
   s.y = (int16_t)c.y;
   s.lw = (uint8_t)ilog2(c.w);
   s.lh = (uint8_t)ilog2(c.h);
   s.align = (uint8_t)c.align;
   s.outOff = (uint16_t)c.outOff;
-  s.sbBase = (uint16_t)sbBase;
 }
 
 // Cooperative item: tasks of CUs of one size, each CU spanning nsb >= 64
@@ -150,7 +149,7 @@ Item make_coop_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& task
     for (auto& c : tasks[t])
       if (nsb_of(c) != nsb) abort();
     if (nsb < 64 || n * nsb > threads || n > stride) abort();
-    for (int i = 0; i < n; i++) set_slot(it.cu[t * stride + i], tasks[t][i], i * nsb);
+    for (int i = 0; i < n; i++) set_slot(it.cu[t * stride + i], tasks[t][i]);
     it.cu[t * stride].taskCus = (uint8_t)n;
     it.cu[t * stride].taskLogL = (uint16_t)ilog2(nsb);
     it.nCu = (int16_t)(t * stride + n);
@@ -183,7 +182,7 @@ Item make_auto_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& task
     for (auto& c : tasks[t])
       if (nsb_of(c) != nsb) abort();
     if (n * nsb > 64 || nsb < 16 || n > kTaskCu) abort();  // the kernel's segment sums handle 16 / 32 / 64
-    for (int i = 0; i < n; i++) set_slot(it.cu[t * kTaskCu + i], tasks[t][i], i * nsb);
+    for (int i = 0; i < n; i++) set_slot(it.cu[t * kTaskCu + i], tasks[t][i]);
     it.cu[t * kTaskCu].taskCus = (uint8_t)n;
     it.cu[t * kTaskCu].taskLogL = (uint16_t)ilog2(nsb);
   }

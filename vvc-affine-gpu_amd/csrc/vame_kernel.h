@@ -58,7 +58,7 @@ struct CuSlot {          // 8 bytes
   uint8_t taskCus : 5;   // a task's first slot: CUs in the task (0 elsewhere)
   uint16_t outOff : 9;   // RETURN_STRIDE[group] + cuIdx
   uint16_t taskLogL : 4;  // a task's first slot: log2 lanes per CU
-  uint16_t sbBase;       // first sub-block of this CU in its task (prediction rows; autonomous tasks: + 64 * wave)
+  uint16_t pad;
 };
 static_assert(sizeof(CuSlot) == 8, "CuSlot packing");
 
@@ -1635,7 +1635,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       g.h = 1 << g.lh;
       g.x = ctuX + cs.x;
       g.y = ctuY + cs.y;
-      sbIdx = (coop ? 0 : wv * 64) + cs.sbBase + local;  // autonomous: the running wave's rows
+      // the lane's own prediction rows: a task's CUs take consecutive lanes
+      // (of the workgroup, or of the running wave), in raster order within each
+      sbIdx = tid;
       sbCols = 1 << (g.lw - 2);
       sx = (local & (sbCols - 1)) << 2;
       sy = (local >> (g.lw - 2)) << 2;
@@ -2007,7 +2009,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       }
       if constexpr (run3) run_pass(I3{}, F{}, F{});
     }
-    if (!C::AUTO) break;
+    if (KIND == kKindHalf) break;  // one CU per item
     // the next task's CU slots into this task's (cooperative: after every wave's
     // last read of them, autonomous: the wave's own, read by this wave only)
     int next = task + (coop ? 1 : 4);
@@ -2018,10 +2020,10 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     }
     if (next >= nTasks) break;
     if (coop) {
-      if (tid < kTaskCu) s_cu[tid] = s_cu[min(next, kMaxTasks - 1) * kTaskCu + tid];
+      if (tid < kTaskCu) s_cu[tid] = s_cu[min(next, C::ITEMCU / kTaskCu - 1) * kTaskCu + tid];
       __syncthreads();
     } else {
-      if (lane < kTaskCu) s_cu[wv * kTaskCu + lane] = s_cu[min(next, kMaxTasks - 1) * kTaskCu + lane];
+      if (lane < kTaskCu) s_cu[wv * kTaskCu + lane] = s_cu[min(next, C::ITEMCU / kTaskCu - 1) * kTaskCu + lane];
       wave_sync();
     }
     task = next;
