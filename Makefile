@@ -12,7 +12,12 @@ LIBDIR  := $(PKG)/lib
 BINDIR  := $(PKG)/bin
 # -ffp-contract=off: the FP64 solve must round exactly like the reference
 # (explicit fma where OpenCL's FP_CONTRACT fuses); integer paths are unaffected.
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+# -disable-machine-licm: the quadrant kernel's task loop (several tasks per
+# workgroup) made MachineLICM hoist constants and lane addresses out of it and
+# spill registers for them (16-48 B/lane, their writes reaching HBM); without
+# it every kernel runs at zero scratch.
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
+            -mllvm -disable-machine-licm
 
 LIB_SRCS := $(CSRC)/vame_engine.hip $(CSRC)/vame_hostlogic.cpp $(CSRC)/vame_io.cpp
 LIB_HDRS := $(CSRC)/vame_kernel.h $(CSRC)/vame_tables.h include/vame.h

@@ -335,6 +335,8 @@ def main():
                      "profile": prof.get("profile"),
                      "profiled_workload": prof.get("profiled_workload"),
                      "profile_matches_workload": profile_matches(prof, cfg, run, world, args.rank_only),
+                     # and whether it was taken with the library this line loaded
+                     "profile_same_library": profile_same_library(prof),
                      "alg_bytes_per_launch": quad_bytes / max(quad_n, 1),
                      # fraction of the algorithmic sub-block predictions the exact
                      # early exit actually runs (instrumented build, profiles/)
@@ -399,6 +401,15 @@ def profile_matches(prof: dict, cfg: dict, run, world: int, rank_only) -> bool |
     return (pw.get("resolution") == f"{cfg['W']}x{cfg['H']}" and pw.get("qp") == cfg["qp"]
             and pw.get("modes") == ("2cp+3cp" if cfg["modes"] & 2 else "2cp")
             and pw.get("pairs_per_step_rank0") == run.pairs and pw.get("rank_only") == ro)
+
+
+def profile_same_library(prof: dict) -> bool | None:
+    """Whether the committed profile's run loaded the same HIP library (its
+    sha256) as this line: its kernel times describe this build's kernels."""
+    pw = prof.get("profiled_workload") or {}
+    if not pw.get("native_sha256"):
+        return None
+    return pw["native_sha256"] == native_record()["sha256"]
 
 
 def load_profile(config: str, avg_launch_ms: float) -> dict:

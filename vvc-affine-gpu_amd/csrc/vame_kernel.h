@@ -1489,7 +1489,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   __shared__ long long s_dup[(VAME_DUP & 4) ? kNumMom : 1];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wv = tid >> 6;
+  const int wv = tid >> 6;
   constexpr int ph_off = 0;  // phase-timing slots (3-CP pass: +kNumPhases)
   (void)ph_off;
   PH_DECL
@@ -1608,7 +1608,14 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   // wv * kTaskCu .. (autonomous: its CU state, moments and systems; its
   // sub-blocks use the wave's own prediction rows, so its tasks need no
   // workgroup barrier).
+  const int tidItem = tid;
   for (int task = coop ? 0 : __builtin_amdgcn_readfirstlane(wv);;) {
+    // the thread's ids re-derived per task (opaque): as values carried
+    // around the task loop, everything computed from them was hoisted out of
+    // it and held in spill slots, whose writes reached HBM
+    int tidTask = tidItem;
+    opaque(tidTask);
+    const int tid = tidTask, lane = tid & 63, wv = tid >> 6;
     // ---- CUs of this wave, this lane's CU and sub-blocks (fixed for the task)
     const int lidx = coop ? tid : lane;
     const CuSlot t0 = s_cu[coop ? 0 : wv * kTaskCu];
@@ -2009,7 +2016,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       }
       if constexpr (run3) run_pass(I3{}, F{}, F{});
     }
-    if (KIND == kKindHalf) break;  // one CU per item
+    if (KIND != kKindQuad) break;  // 128-class items: one task
     // the next task's CU slots into this task's (cooperative: after every wave's
     // last read of them, autonomous: the wave's own, read by this wave only)
     int next = task + (coop ? 1 : 4);
