@@ -1489,6 +1489,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   __shared__ long long s_dup[(VAME_DUP & 4) ? kNumMom : 1];
 
   const int tid = threadIdx.x;
+  [[maybe_unused]] const int lane = tid & 63;  // (the phase-timing macros)
   const int wv = tid >> 6;
   constexpr int ph_off = 0;  // phase-timing slots (3-CP pass: +kNumPhases)
   (void)ph_off;
