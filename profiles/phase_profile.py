@@ -7,6 +7,10 @@
 Runs bench.py's workload, then prints, per kernel, the share of wave-clock
 spent in each phase (summed over all waves: it weights phases by how long
 waves sit in them, including barrier / wave-sync waits at the phase's end).
+Since the quadrant items run several tasks (round 4), the timing registers
+push this build's 3-CP quadrant instances past 128 VGPRs (3 waves per SIMD
+instead of 4): their shares describe a slower kernel; the 2-CP-only (c2)
+instance keeps 4.
 """
 import argparse
 import ctypes
