@@ -68,7 +68,7 @@ typedef struct {
  * VAME_TASKS (wave tasks per autonomous quadrant item, 1..16, default 16),
  * VAME_CLAIM, VAME_CHAIN, VAME_MIX (default 1 each), VAME_HALF128,
  * VAME_HALF_MIN_PAIRS; launch structure VAME_STREAMS, VAME_QUAD_FIRST,
- * VAME_GRAPH, VAME_JOIN_EACH; block order VAME_XCD_ORDER, VAME_GROUP_COMBOS,
+ * VAME_GRAPH, VAME_JOIN_EACH; block order VAME_ITEM_ORDER, VAME_XCD_ORDER, VAME_GROUP_COMBOS,
  * VAME_GROUP_COMBOS_BIG. */
 int vame_create(vame_ctx** out, int device, int width, int height);
 void vame_destroy(vame_ctx* ctx);

@@ -430,11 +430,11 @@ def test_property_translation_1080p(engines, d):
                                  {"VAME_GRAPH": "1"}, {"VAME_GRAPH": "1", "VAME_HALF128": "1"},
                                  {"VAME_GRAPH": "1", "VAME_STREAMS": "2"}, {"VAME_MIX": "0"},
                                  {"VAME_TASKS": "8"}, {"VAME_TASKS": "4", "VAME_CHAIN": "0", "VAME_MIX": "0"},
-                                 {"VAME_TASKS": "1"}, {"VAME_CLAIM": "0"}],
+                                 {"VAME_TASKS": "1"}, {"VAME_CLAIM": "0"}, {"VAME_ITEM_ORDER": "0"}],
                          ids=["half512_packing", "ctu1024_packing", "two_streams", "two_streams_half512",
                               "ctu_first", "graph", "graph_half512", "graph_two_streams", "aligns_unmixed",
                               "items_of_8", "items_of_4_unchained_unmixed", "items_of_1_task",
-                              "static_tasks"])
+                              "static_tasks", "items_by_quadrant"])
 def test_launch_structure_variants(env, monkeypatch):
     """The engine's launch-structure knobs (read at vame_create) change only
     where the work runs: VAME_HALF128=1 gives every 128x64 / 64x128 CU a
@@ -449,7 +449,8 @@ def test_launch_structure_variants(env, monkeypatch):
     task as it finishes; VAME_CLAIM=0: wave w runs tasks w, w + 4, ...),
     VAME_CHAIN=0 gives each cooperative group an item of its own instead of
     one chained cooperative item per quadrant, VAME_MIX=0 runs a launch of
-    both alignments on the two alignments' own items; VAME_GRAPH=1 captures a call's launches
+    both alignments on the two alignments' own items, VAME_ITEM_ORDER=0 lists
+    the autonomous items quadrant by quadrant; VAME_GRAPH=1 captures a call's launches
     into a hipGraph and replays it when the call repeats (each call below runs
     twice, the second from the graph, after its outputs were cleared).  A 1080p
     POC with 2 refs (2+3 CP) and a 2-CP-only POC give the default context's

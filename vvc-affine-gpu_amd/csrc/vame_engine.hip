@@ -245,6 +245,7 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& halfItems, std::
     }
   }
   std::vector<Item> bothCoop, bothAuto;
+  std::vector<int> autoRank;  // an autonomous item's index within its quadrant
   for (int q = 0; q < 4; q++) {
     const int qx = (q & 1) * 64, qy = (q >> 1) * 64;
     auto inq = [&](int x, int y) { return x >= qx && x < qx + 64 && y >= qy && y < qy + 64; };
@@ -288,12 +289,24 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& halfItems, std::
       coop(t, bothCoop);
       std::vector<CuDesc> small(fullSmall);
       small.insert(small.end(), halfSmall.begin(), halfSmall.end());
+      const size_t n0 = bothAuto.size();
       pack_autonomous(qx, qy, small, bothAuto, tasks);
+      for (size_t k = n0; k < bothAuto.size(); k++) autoRank.push_back((int)(k - n0));
     }
   }
   if (mixed) {
     quadBoth = bothCoop;
-    quadBoth.insert(quadBoth.end(), bothAuto.begin(), bothAuto.end());
+    // every quadrant's first (largest-task) autonomous item, then the seconds,
+    // ...: the kernel's last workgroups are its shortest (VAME_ITEM_ORDER=0:
+    // quadrant by quadrant)
+    if (env_int("VAME_ITEM_ORDER", 1) == 1) {
+      std::vector<size_t> idx(bothAuto.size());
+      for (size_t k = 0; k < idx.size(); k++) idx[k] = k;
+      std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return autoRank[a] < autoRank[b]; });
+      for (size_t k : idx) quadBoth.push_back(bothAuto[k]);
+    } else {
+      quadBoth.insert(quadBoth.end(), bothAuto.begin(), bothAuto.end());
+    }
   } else {
     quadBoth = quadFull;
     quadBoth.insert(quadBoth.end(), quadHalf.begin(), quadHalf.end());
