@@ -22,7 +22,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
 LIB_SRCS := $(CSRC)/vame_engine.hip $(CSRC)/vame_hostlogic.cpp $(CSRC)/vame_io.cpp
 LIB_HDRS := $(CSRC)/vame_kernel.h $(CSRC)/vame_tables.h include/vame.h
 
-all: lib cli synth oracle
+all: lib cli synth oracle probe
 
 lib: $(LIBDIR)/libvame.so
 
@@ -52,6 +52,11 @@ phase:
 
 cli: $(BINDIR)/vame
 
+# does an event after a call wait for its any-order kernels? (tests/test_gpu_parity.py)
+probe: tests/native/anyorder_probe
+tests/native/anyorder_probe: tests/native/anyorder_probe.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -Wall -o $@ $<
+
 $(LIBDIR)/libvame.so: $(LIB_SRCS) $(LIB_HDRS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(LIB_SRCS)
@@ -72,4 +77,4 @@ clean:
 	rm -rf $(LIBDIR) $(BINDIR)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all lib cli synth oracle clean resource-usage ablate phase variant count
+.PHONY: all lib cli synth oracle probe clean resource-usage ablate phase variant count

@@ -28,9 +28,19 @@ frames of its own share, with no collective on the data path.
   c5           scales strongly: 240 POCs of 3840x2160 in all (configs[4]),
                contiguous pair blocks of one sequence.
 After the timed steps the decision records go to rank 0 in one RCCL gather
-(timed and reported separately as `gather`), and rank 0 recomputes the first
-and last POC of every rank's block and checks the gathered records byte for
-byte.  Rank 0 prints one JSON line.
+(pack and exchange timed apart and reported as `gather`), and rank 0
+recomputes the first and last POC of every rank's block and checks the
+gathered records byte for byte.  Every line (N = 1 too) then carries
+`frame_shard`: north star's frame shard of ONE 3840x2160 sequence
+(--fs-frames, default 48 POCs = 186 pairs) over the N ranks with the gather
+into rank 0 inside its timed span.  Rank 0 prints one JSON line.
+
+`roofline`: the dominant kernel (affine_me_quad) is VALU-issue
+bound; `frac` = SQ_INSTS_VALU per launch (committed rocprofv3 profile of the
+config, profiles/pmc_<config>.json) over the live launch time and the wave64
+issue ceiling.  The HBM views ride beside it: measured traffic, the
+algorithmic bytes of the executed predictions (`hbm_executed_frac`), and the
+survey's algorithmic-byte ratio (`alg_byte_ratio`, a throughput score).
 """
 from __future__ import annotations
 
@@ -59,6 +69,10 @@ CONFIGS = {
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 N_SIMD = 1024          # 256 CUs x 4 SIMDs
+# VALU issue ceiling: a wave64 VALU instruction issues over 2 cycles on a
+# 32-wide SIMD (MI355X_MICROARCH.md), 0.5 wave-instructions per SIMD-cycle, at
+# the 2.4 GHz peak engine clock: 1,228.8 G wave-instructions/s
+VALU_PEAK_GINST = N_SIMD * 2.4 * 0.5
 
 
 def log(*a):
@@ -85,6 +99,9 @@ def main():
                          "(no process group, no gather): one rank of an N-GPU node, priced on one GPU")
     ap.add_argument("--no-spans", action="store_true",
                     help="skip the per-POC span step (profiling runs: identical launches only)")
+    ap.add_argument("--fs-frames", type=int, default=48,
+                    help="frames of the 2160p sequence the `frame_shard` record codes over the ranks "
+                         "(0 = no record)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     args.steps = cfg["steps"] if args.steps is None else args.steps
@@ -163,9 +180,9 @@ def main():
         run.step()
     barrier()
     # HIP events on the dominant (quadrant) kernel's dispatches of the timed
-    # steps; the 128-class kernel is timed on extra steps after them (timing
-    # its dispatches too cost ~0.7 % of a c2 step).  Diagnostic override
-    # VAME_BENCH_KTIMING: 0 = no events, 1 = both kernels in the timed steps.
+    # steps; the 128-class kernels are timed on extra steps after them (timing
+    # their dispatches too cost ~0.7 % of a c2 step).  Diagnostic override
+    # VAME_BENCH_KTIMING: 0 = no events, 1 = every kernel in the timed steps.
     ktiming = int(os.environ.get("VAME_BENCH_KTIMING", "2"))
     # the events ride on a sample of the timed steps -- every ksample-th step
     # (VAME_BENCH_KSAMPLE, default 4) -- so the timed span carries a quarter of
@@ -173,32 +190,36 @@ def main():
     # ~0.7 % of a c2 step)
     ksample = max(1, int(os.environ.get("VAME_BENCH_KSAMPLE", "4")))
     eng.set_timing(ktiming)
-    # the per-step spread: HIP events around the sampled steps only (an event
-    # record is a marker packet between two steps' kernels); VAME_BENCH_STEPEV=all
-    # brackets every step
+    # the per-step spread: HIP events around the steps that carry no kernel
+    # events (i % ksample == 1; an event record is a marker packet between two
+    # steps' kernels), so the spread describes a plain timed step;
+    # VAME_BENCH_STEPEV=all brackets every step
     every_step = os.environ.get("VAME_BENCH_STEPEV", "sampled") == "all"
     step_ev = []
     t_start = time.perf_counter()
     for i in range(args.steps):
         sampled = i % ksample == 0
+        bracket = every_step or (i % ksample == (1 if ksample > 1 else 0))
         if ksample > 1:
             eng.set_timing(ktiming if sampled else 0, keep=True)
-        if every_step or sampled:
+        if bracket:
             a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a_.record()
         run.step()
-        if every_step or sampled:
+        if bracket:
             b_.record()
             step_ev.append((a_, b_))
     barrier()
     elapsed = time.perf_counter() - t_start
     step_ms = sorted(a_.elapsed_time(b_) for a_, b_ in step_ev)
+    if not step_ms:  # fewer timed steps than one sample period
+        step_ms = [elapsed * 1e3 / max(args.steps, 1)]
     quad_ms, quad_n = eng.get_timing(0)
     # the 128-class kernels (128x128 CUs: affine_me_ctu, class 1; 128x64 /
-    # 64x128 CUs: affine_me_half, class 2), timed in the timed steps only with
-    # VAME_BENCH_KTIMING=1, else on extra untimed steps after them
+    # 64x128 CUs: affine_me_half, class 2), timed in the sampled timed steps
+    # with VAME_BENCH_KTIMING=1, else on extra untimed steps after them
     big_t = {k: eng.get_timing(k) for k in (1, 2)}
-    big_on, big_steps = "timed steps", args.steps
+    big_on = "the sampled timed steps"
     if ktiming != 1:
         big_steps = min(args.steps, 20)
         eng.set_timing(True)
@@ -227,33 +248,47 @@ def main():
     value = rows_total / tmax
 
     # the one exchange step, outside the timed steps: decision records to rank 0
-    # (a --rank-only diagnostic has no other ranks: it checks its own block)
-    barrier()
-    tg = time.perf_counter()
+    # (a --rank-only diagnostic has no other ranks: it checks its own block).
+    # The pack runs once untimed first (its kernels' first use), then pack and
+    # exchange are timed apart, each between barriers.
+    gather_rec = {"to": "rank 0", "backend": "none" if dist is None else dist.get_backend()}
     if args.rank_only is None:
-        slabs, gather_bytes = run.gather()
+        run.slab()
+        barrier()
+        tg = time.perf_counter()
+        slab = run.slab()
+        torch.cuda.synchronize()
+        pack_ms = (time.perf_counter() - tg) * 1e3
+        barrier()
+        tg = time.perf_counter()
+        slabs, gather_bytes = run.exchange(slab)
+        torch.cuda.synchronize()
+        exch_ms = (time.perf_counter() - tg) * 1e3
+        del slab
+        pack_ms, exch_ms = all_reduce([pack_ms, exch_ms], ops and ops.MAX)
+        gather_rec.update({"pack_ms": pack_ms, "exchange_ms": exch_ms, "bytes_into_rank0": gather_bytes,
+                           "exchange_GBps": gather_bytes / exch_ms / 1e6 if gather_bytes and exch_ms > 0
+                           else None})
+        gather_rec["check"] = run.verify(slabs) if rank == 0 else None
+        del slabs
     else:
-        slabs, gather_bytes = None, 0
-    torch.cuda.synchronize()
-    gather_ms = (time.perf_counter() - tg) * 1e3
-    gather_ms = all_reduce([gather_ms], ops and ops.MAX)[0]
-    if args.rank_only is not None:
-        check = run.verify_own()
-    else:
-        check = run.verify(slabs) if rank == 0 else None
-    del slabs
+        gather_rec.update({"pack_ms": None, "exchange_ms": None, "bytes_into_rank0": 0,
+                           "check": run.verify_own()})
 
-    # roofline of the dominant kernel (quadrant work items, affine_me_quad)
-    # the algorithmic bytes of the timed steps whose quadrant dispatches carried
-    # events (every ksample-th; each step is `launches_per_step` launches)
+    # the kernels' time per launch (sampled HIP events on their own dispatches)
     launches_per_step = -(-run.pairs // 32)
-    quad_bytes = acc["bytes_quad"] * run.pairs * (quad_n / launches_per_step)
-    achieved = quad_bytes / (quad_ms * 1e-3) / 1e9 if quad_ms > 0 else 0.0
-    # per 128-class kernel: its dispatches' average and the algorithmic bytes
-    # it carries: with affine_me_half launches (a launch of >= 16 pairs, the
-    # engine's default) the CTU items hold only the 128x128 CUs; otherwise all
-    # 128-class CUs (a mix of both packings in one step leaves the CTU kernel's
-    # bytes unattributed)
+    prof = load_profile(args.config)
+    pc = prof.get("pred_count") or {}
+    # the algorithmic bytes of one launch of each kernel class (per launch:
+    # the launches of a step split its pairs; the events' launches are counted)
+    per_launch = lambda key: acc[key] * run.pairs / launches_per_step  # noqa: E731
+    quad_avg = quad_ms / quad_n if quad_n else 0.0
+    roof_q = kernel_roof(quad_avg, per_launch("bytes_quad"), prof.get("kernels", {}).get("affine_me_quad"),
+                         pc.get("executed_pred_frac_quad"))
+    # per 128-class kernel: with affine_me_half launches (a launch of >= 16
+    # pairs, the engine's default) the CTU items hold only the 128x128 CUs;
+    # otherwise all 128-class CUs (a mix of both packings in one step leaves
+    # the CTU kernel's bytes unattributed)
     split = big_t[2][1] > 0
     mixed = split and big_t[2][1] != big_t[1][1]
     big_kernels = {}
@@ -262,17 +297,75 @@ def main():
         ms, n = big_t[k]
         if n == 0 or (mixed and k == 1):
             continue
-        b = acc[key] * run.pairs * big_steps
-        ach = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-        big_kernels[name] = {
-            "timed_on": big_on, "avg_launch_ms": ms / n, "launches": n, "alg_bytes_per_launch": b / n,
-            # algorithmic bytes over the dispatch's span, which runs beside the
-            # quadrant kernel and waits for CUs it frees: a residency span, not
-            # this kernel's efficiency (the whole step's figure is `step_frac`)
-            "resident_span_GBps": ach, "resident_span_frac": ach / HBM_PEAK_GBS}
+        big_kernels[name] = {"timed_on": big_on, "launches": n,
+                             **kernel_roof(ms / n, per_launch(key), prof.get("kernels", {}).get(name),
+                                           pc.get("executed_pred_frac_ctu"))}
     step_bytes = acc["bytes"] * run.pairs
-    span_achieved = step_bytes / (span_ms * 1e-3) / 1e9 if span_ms > 0 else 0.0
-    prof = load_profile(args.config, quad_ms / max(quad_n, 1))
+    span_alg = step_bytes / (span_ms * 1e-3) / 1e9 if span_ms > 0 else 0.0
+    # the whole timed step: every kernel's VALU instructions (profiled per
+    # launch) and algorithmic bytes over the step's time
+    step_s = elapsed / args.steps
+    step_insts = None
+    if roof_q.get("insts_valu_per_launch") is not None:
+        step_insts = roof_q["insts_valu_per_launch"] * launches_per_step
+        for name, r in big_kernels.items():
+            if r.get("insts_valu_per_launch") is None:
+                step_insts = None
+                break
+            step_insts += r["insts_valu_per_launch"] * launches_per_step
+    step_alg = step_bytes / step_s / 1e9 / HBM_PEAK_GBS if step_s > 0 else 0.0
+
+    roofline = {
+        # the binding resource (rocprofv3 SQ counters, profiles/pmc_<config>.json):
+        # VALU issue -- SQ_INSTS_VALU per launch over this run's launch time,
+        # against the wave64 issue ceiling of 1,024 SIMDs at the peak clock
+        "bound": "valu",
+        "kernel": "affine_me_quad",
+        "achieved": roof_q.get("valu_Ginst_per_s"),
+        "peak": VALU_PEAK_GINST,
+        "unit": "G VALU wave-instructions/s",
+        "frac": roof_q.get("valu_frac"),
+        # SQ_ACTIVE_INST_VALU: the VALU pipe's busy cycles (most of the kernel's
+        # instructions hold it for more than the 2 issue cycles)
+        "busy": roof_q.get("valu_busy"),
+        # measured HBM bytes per launch (PMC FETCH_SIZE x 2 + WRITE_SIZE)
+        "traffic": roof_q.get("hbm_bytes_per_launch"),
+        "hbm_measured_frac": roof_q.get("hbm_measured_frac"),
+        # the prescribed HBM view: the algorithmic window bytes of
+        # the predictions the exact early exit runs, over the launch time and
+        # 8 TB/s; and the same for every algorithmic prediction -- a throughput
+        # score (it exceeds 1 once the early exit skips enough), not a fraction
+        "hbm_executed_frac": roof_q.get("hbm_executed_frac"),
+        "alg_byte_ratio": roof_q.get("alg_byte_ratio"),
+        "executed_pred_frac": pc.get("executed_pred_frac_quad"),
+        "avg_launch_ms": quad_avg,
+        "launches": quad_n,
+        # the timed steps whose quadrant dispatches carry the events
+        "timed_sample": {"every": ksample, "steps": len(range(0, args.steps, ksample)) if ktiming else 0,
+                         "launches_per_step": launches_per_step},
+        "alg_bytes_per_launch": roof_q["alg_bytes_per_launch"],
+        "insts_valu_per_launch": roof_q.get("insts_valu_per_launch"),
+        "wave_cycle_split": roof_q.get("wave_cycle_split"),
+        # the same kernel's average under rocprofv3 over the timed dispatches
+        # of a traced run of this config, the committed profile the counter
+        # fields come from, the workload it was taken on, whether that is this
+        # line's workload and whether it ran the library this line loaded
+        "rocprof_avg_ms": (prof.get("kernels", {}).get("affine_me_quad") or {}).get("timed_avg_ms"),
+        "profile": prof.get("profile"),
+        "profiled_workload": prof.get("profiled_workload"),
+        "profile_matches_workload": profile_matches(prof, cfg, run, world, args.rank_only),
+        "profile_same_library": profile_same_library(prof),
+        **big_kernels,
+        # every kernel of the timed step together
+        "step": {"valu_frac": (step_insts / step_s / 1e9 / VALU_PEAK_GINST) if step_insts and step_s > 0
+                 else None,
+                 "hbm_executed_frac": step_alg * pc["executed_pred_frac"] if pc.get("executed_pred_frac")
+                 else None,
+                 "alg_byte_ratio": step_alg},
+        "fused_poc_launch": {"alg_byte_ratio": span_alg / HBM_PEAK_GBS,
+                             "avg_launch_ms": span_ms / max(span_n, 1),
+                             "alg_bytes_per_launch": step_bytes / max(span_n, 1)},
+    }
 
     result = {
         "metric": "candidate CU-blocks/s at 1080p QP32; bit-exact CPMV/cost match vs reference",
@@ -283,7 +376,8 @@ def main():
         "warmup": args.warmup,
         "prewarm": {"seconds": args.prewarm_s, "steps": prewarm_steps},
         "ms_per_step": tmax * 1e3 / args.steps,
-        # rank 0's per-step GPU times (HIP events around the sampled steps)
+        # rank 0's per-step GPU times (HIP events around the timed steps that
+        # carry no kernel-timing events)
         "step_ms": {"median": step_ms[len(step_ms) // 2], "min": step_ms[0], "max": step_ms[-1],
                     "steps": len(step_ms)},
         "world": {"size": world, "backend": "none" if dist is None else dist.get_backend(),
@@ -296,7 +390,8 @@ def main():
         # which multi-GPU form this line measures: weak scaling over
         # independent sequences ("streams", the default) or over pair blocks
         # of one sequence ("sequence"); c5 is the north star's frame shard of
-        # one 240-frame sequence (strong scaling)
+        # one 240-frame sequence (strong scaling); every line also carries the
+        # frame shard of one 2160p sequence (`frame_shard`)
         "scaling_form": ("streams" if streams else "sequence") if weak else "frame-shard",
         "vs_baseline": None,
         "dtype": "int32",
@@ -311,65 +406,37 @@ def main():
                                    f"frame-shard x{world} (pair_shard of one sequence)"),
                    "scaling_form_note": ("N independent sequences (each rank codes the 1-GPU config "
                                          "on its own synthetic sequence); the frame shard of one "
-                                         "sequence is --config c5" if streams else
+                                         "sequence is `frame_shard` (and --config c5)" if streams else
                                          "the first P x N pairs of one sequence in contiguous pair "
                                          "blocks (deeper POCs on higher ranks)" if weak else
                                          "240 POCs of one sequence in contiguous pair blocks over "
                                          "the ranks"),
                    **({"rank_only": {"rank": rank, "of": world}} if args.rank_only is not None else {})},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": prof.get("traffic"),
-                     "kernel": "affine_me_quad",
-                     "avg_launch_ms": quad_ms / max(quad_n, 1),
-                     "launches": quad_n,
-                     # the timed steps whose quadrant dispatches carry the events
-                     "timed_sample": {"every": ksample,
-                                      "steps": len(range(0, args.steps, ksample)) if ktiming else 0,
-                                      "launches_per_step": launches_per_step},
-                     # the same kernel's average under rocprofv3 over the timed
-                     # dispatches of a traced run of this config (profiles/)
-                     "rocprof_avg_ms": prof.get("rocprof_avg_ms"),
-                     # the committed profile the rocprof / counter fields come
-                     # from, the workload it was taken on, and whether that is
-                     # this line's workload
-                     "profile": prof.get("profile"),
-                     "profiled_workload": prof.get("profiled_workload"),
-                     "profile_matches_workload": profile_matches(prof, cfg, run, world, args.rank_only),
-                     # and whether it was taken with the library this line loaded
-                     "profile_same_library": profile_same_library(prof),
-                     "alg_bytes_per_launch": quad_bytes / max(quad_n, 1),
-                     # fraction of the algorithmic sub-block predictions the exact
-                     # early exit actually runs (instrumented build, profiles/)
-                     "executed_pred_frac": prof.get("executed_pred_frac"),
-                     # the kernel's real bound: VALU issue (rocprofv3 SQ counters, profiles/)
-                     "valu": prof.get("valu"),
-                     # every kernel's algorithmic bytes over the whole timed step
-                     "step_frac": acc["bytes"] * run.pairs * args.steps / (elapsed * 1e9) / HBM_PEAK_GBS
-                     if elapsed > 0 else 0.0,
-                     **big_kernels,
-                     "fused_poc_launch": {"achieved": span_achieved,
-                                          "frac": span_achieved / HBM_PEAK_GBS,
-                                          "avg_launch_ms": span_ms / max(span_n, 1),
-                                          "alg_bytes_per_launch": step_bytes / max(span_n, 1)}},
+        "roofline": roofline,
         # SURVEY §8(d) companions: in-frame candidates (the rows the kernels
         # predict; out-of-frame rows are logged with their initial cost) and the
         # compulsory bytes (orig + ref frame + results per pair) over the step
         "value_inframe": inframe_total / tmax,
         "compulsory": {"bytes_per_step_all": compulsory_total / args.steps,
                        "GBps": compulsory_total / tmax / 1e9 if tmax > 0 else 0.0},
-        "gather": {"to": "rank 0", "backend": "none" if dist is None else dist.get_backend(),
-                   "ms": gather_ms, "bytes_into_rank0": gather_bytes,
-                   "check": check},
+        "gather": gather_rec,
     }
-
     result["native"] = native_record()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"], result["parity_sample"] = cpu_baseline(run, acc, ncps, W, H, modes)
+    eng.close()
+    del run
+    torch.cuda.empty_cache()
+    # north star's frame shard of one sequence, with the RCCL gather of the
+    # decision records into rank 0 inside its timed span (every N, N = 1 too;
+    # a c5 line is that shard itself, over the whole 240 frames)
+    if args.fs_frames > 0 and args.rank_only is None and args.config != "c5":
+        result["frame_shard"] = frame_shard_record(args.fs_frames, dist, rank, world, dev, barrier,
+                                                   all_reduce, ops)
     if dist is not None:
         dist.barrier()
     if rank == 0 or args.rank_only is not None:
         print(json.dumps(result), flush=True)
-    eng.close()
     if dist is not None:
         dist.destroy_process_group()
 
@@ -412,35 +479,117 @@ def profile_same_library(prof: dict) -> bool | None:
     return pw["native_sha256"] == native_record()["sha256"]
 
 
-def load_profile(config: str, avg_launch_ms: float) -> dict:
-    """Counter-derived figures for the quadrant kernel from the committed
-    profile of this config (profiles/pmc_<config>.json, written by
-    profiles/pmc_summary.py from rocprofv3 passes over identical launches):
-      traffic             HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE)
-      valu                VALU issue: SQ_INSTS_VALU per launch over the SIMD
-                          cycles of this run's launch time at the profiled clock
-      executed_pred_frac  sub-block predictions run / algorithmic count"""
+def load_profile(config: str) -> dict:
+    """The committed counter profile of this config (profiles/pmc_<config>.json,
+    written by profiles/pmc_summary.py from rocprofv3 passes over identical
+    launches): per kernel its rocprof timed average, HBM bytes per launch
+    (FETCH_SIZE x 2 + WRITE_SIZE), SQ counters per launch (SQ_INSTS_VALU, ...)
+    and VALU busy fraction; the executed-prediction count of the
+    instrumentation build; the workload and library it was taken with."""
     path = os.path.join(REPO, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
         return {}
     p = json.load(open(path))
-    out = {"traffic": p.get("quad_hbm_bytes_per_launch"),
-           "executed_pred_frac": p.get("executed_pred_frac"),
-           "rocprof_avg_ms": p.get("quad_timed_avg_ms_rocprof"),
-           "profiled_workload": p.get("profiled_workload"),
-           "profile": os.path.relpath(path, REPO)}
-    sq = p.get("quad_sq")
-    if sq and avg_launch_ms > 0:
-        clk = sq["clock_ghz"]
-        cycles = avg_launch_ms * 1e-3 * clk * 1e9
-        rate = sq["insts_valu_per_launch"] / (N_SIMD * cycles)
-        out["valu"] = {"insts_valu_per_launch": sq["insts_valu_per_launch"],
-                       "issue_rate": rate, "peak_issue_rate": sq["peak_issue_rate"],
-                       "frac": rate / sq["peak_issue_rate"],
-                       "busy_frac_profiled": sq["valu_busy"],
-                       "clock_ghz_profiled": clk,
-                       "unit": "VALU wave-instructions per SIMD-cycle"}
+    return {"kernels": p.get("kernels", {}), "pred_count": p.get("pred_count"),
+            "profiled_workload": p.get("profiled_workload"), "profile": os.path.relpath(path, REPO)}
+
+
+def kernel_roof(avg_ms: float, alg_bytes: float, prof_kernel: dict | None, exec_frac: float | None) -> dict:
+    """One kernel's roofline figures from its live launch time and its
+    committed profile:
+      valu_frac          SQ_INSTS_VALU per launch / (avg launch time x the wave64
+                         issue ceiling of 1,024 SIMDs at the 2.4 GHz peak clock:
+                         0.5 wave-instructions per SIMD-cycle) -- the bound
+      valu_busy          SQ_ACTIVE_INST_VALU x 4 / (1,024 SIMD x GPU cycles), profiled
+      hbm_measured_frac  measured HBM bytes per launch / time / 8 TB/s
+      hbm_executed_frac  algorithmic bytes x executed-prediction fraction / time / 8 TB/s
+      alg_byte_ratio     algorithmic bytes / time / 8 TB/s (a throughput score:
+                         it charges predictions the exact early exit skips)"""
+    pk = prof_kernel or {}
+    out = {"avg_launch_ms": avg_ms, "alg_bytes_per_launch": alg_bytes}
+    if avg_ms <= 0:
+        return out
+    alg = alg_bytes / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    out["alg_byte_ratio"] = alg
+    out["hbm_executed_frac"] = alg * exec_frac if exec_frac else None
+    hbm = pk.get("hbm_bytes_per_launch")
+    out["hbm_bytes_per_launch"] = hbm
+    out["hbm_measured_frac"] = hbm / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if hbm else None
+    insts = (pk.get("sq_per_launch") or {}).get("SQ_INSTS_VALU")
+    if insts:
+        g = insts / (avg_ms * 1e-3) / 1e9
+        out.update({"insts_valu_per_launch": insts, "valu_Ginst_per_s": g, "valu_frac": g / VALU_PEAK_GINST,
+                    "valu_busy": pk.get("valu_busy"), "wave_cycle_split": pk.get("wave_cycle_split"),
+                    "rocprof_avg_ms": pk.get("timed_avg_ms")})
     return out
+
+
+def frame_shard_record(n_frames: int, dist, rank: int, world: int, dev, barrier, all_reduce, ops) -> dict:
+    """North star's multi-GPU form at every N: ONE synthetic 3840x2160 QP32
+    sequence of `n_frames` POCs (2- and 3-CP, FULL + HALF) cut into contiguous
+    (POC, refIdx) pair blocks over the ranks (shard.pair_shard), coded with no
+    collective on the data path, and the decision records packed and gathered
+    into rank 0 (RCCL over xGMI) INSIDE the timed span: barrier, then kernels +
+    pack + gather; the span is the max over ranks.  One untimed warm-up pass
+    first (the kernels' first use, clocks).  The gather then runs once more
+    between barriers, timing the exchange alone.  Rank 0 recomputes the first
+    and last block entry of every rank and both halves of every cut POC and
+    compares the gathered records word for word."""
+    from vame.engine import Engine
+    from vame.metrics import pair_accounting
+    from vame.seqrun import ShardRun
+    from vame.shard import sequence_pairs
+    Wf, Hf, qp, modes = 3840, 2160, 32, 3
+    t_syn = time.perf_counter()
+    eng = Engine(Wf, Hf, dev.index)
+    run = ShardRun(eng, Wf, Hf, qp, n_frames, modes, world, rank, dev)
+    syn_s = time.perf_counter() - t_syn
+    acc = pair_accounting(Wf, Hf, (2, 3))
+    run.step()  # untimed warm-up
+    run.slab()
+    barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    run.step()
+    e1.record()
+    slab = run.slab()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    slabs, nbytes = run.exchange(slab)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    kern_ms = e0.elapsed_time(e1)
+    del slabs
+    # the exchange alone, between barriers
+    barrier()
+    t3 = time.perf_counter()
+    slabs, _ = run.exchange(slab)
+    torch.cuda.synchronize()
+    exch_ms = (time.perf_counter() - t3) * 1e3
+    del slab
+    span_ms, kmax, kernels_pack_ms, gather_ms, exch_ms = all_reduce(
+        [(t2 - t0) * 1e3, kern_ms, (t1 - t0) * 1e3, (t2 - t1) * 1e3, exch_ms], ops and ops.MAX)
+    kmin = all_reduce([kern_ms], ops and ops.MIN)[0]
+    check = run.verify(slabs) if rank == 0 else None
+    del slabs
+    total_pairs = sequence_pairs(n_frames)
+    rows = total_pairs * acc["rows"]
+    rec = {"workload": f"{Wf}x{Hf} QP{qp}, {n_frames} frames ({total_pairs} (POC, refIdx) pairs), "
+                       f"2- and 3-CPMV affine (FULL+HALF CUs), contiguous pair blocks of one sequence over "
+                       f"{world} rank(s), decision records gathered into rank 0",
+           "frames": n_frames, "pairs": total_pairs, "pairs_rank0": run.pairs, "rows": rows,
+           "ms": span_ms, "rows_per_s": rows / (span_ms * 1e-3) if span_ms > 0 else None,
+           "kernel_ms": {"max": kmax, "min": kmin},
+           "kernels_pack_ms_max": kernels_pack_ms, "gather_ms_max": gather_ms,
+           "exchange_ms": exch_ms, "bytes_into_rank0": nbytes,
+           "exchange_GBps": nbytes / exch_ms / 1e6 if nbytes and exch_ms > 0 else None,
+           "backend": "none" if dist is None else dist.get_backend(),
+           "synth_s_rank0": syn_s, "check": check}
+    eng.close()
+    del run
+    torch.cuda.empty_cache()
+    return rec
 
 
 def host_cpus():

@@ -15,7 +15,7 @@ O=$R/gpurun_out/$TAG; mkdir -p $O
 for rep in $(seq 1 ${REPS:-2}); do
   for s in "${SETS[@]}"; do
     name=${s%%:*}; vars=${s#*:}
-    env ${vars//,/ } timeout -k 10 ${TMO:-300} python3 $R/bench.py --no-cpu-baseline "$@" \
+    env ${vars//,/ } timeout -k 10 ${TMO:-300} python3 $R/bench.py --no-cpu-baseline --fs-frames 0 "$@" \
         > $O/$name.$rep.json 2> $O/$name.$rep.err || { tail -5 $O/$name.$rep.err; exit 1; }
     python3 - "$O/$name.$rep.json" "$name" <<'PY'
 import json, sys

@@ -12,10 +12,10 @@ tail -c 300 $O/bench_s20.json
 # the other BASELINE configs' lines (c3 / c4 / c5 at N = 1), when asked: bash profiles/run_final.sh all
 if [ "${1:-}" = all ]; then
   for c in c3 c4 c5; do
-    timeout -k 10 400 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
+    timeout -k 10 400 python bench.py --config $c --fs-frames 0 > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
     python -c "
 import json; d=json.loads([l for l in open('$O/bench_$c.json') if l.startswith('{')][-1]); r=d['roofline']
-print('$c', round(d['ms_per_step'], 3), round(d['value'] / 1e6, 1), round(r['frac'], 4), round(r['step_frac'], 4), d.get('parity_sample'))"
+print('$c', round(d['ms_per_step'], 3), round(d['value'] / 1e6, 1), 'valu', r['frac'], 'hbm_exec', r['hbm_executed_frac'], d.get('parity_sample'))"
   done
 fi
 echo final-done

@@ -14,13 +14,13 @@ for v in $VARS; do
   export VAME_GROUP_COMBOS=$G VAME_GROUP_COMBOS_BIG=$GB VAME_XCD_ORDER=$X
   n=g${G}_b${GB}_x${X}
   for cfg in c2 c4; do
-    timeout -k 10 300 python3 $R/bench.py --config $cfg --no-cpu-baseline --no-spans \
+    timeout -k 10 300 python3 $R/bench.py --config $cfg --no-cpu-baseline --fs-frames 0 --no-spans \
         > $O/${cfg}_$n.json 2> $O/${cfg}_$n.err || exit 1
     python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], 'ms/step', round(d['ms_per_step'],3), 'frac', round(d['roofline']['frac'],4), 'quad', round(d['roofline']['avg_launch_ms'],3), 'ctu', round(d['roofline']['affine_me_ctu']['avg_launch_ms'],3), d['gather']['check']['byte_identical'])" $O/${cfg}_$n.json ${cfg}_$n
   done
   [ -n "${NOFETCH:-}" ] && continue
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_$n -o run -- \
-      python3 $R/bench.py --config c4 --no-cpu-baseline --no-spans --steps 2 --warmup 1 > $O/fetch_$n.log 2>&1 || exit 1
+      python3 $R/bench.py --config c4 --no-cpu-baseline --fs-frames 0 --no-spans --steps 2 --warmup 1 > $O/fetch_$n.log 2>&1 || exit 1
   python3 - $O/fetch_$n <<'PY'
 import csv, glob, sys, collections
 acc = collections.defaultdict(list)

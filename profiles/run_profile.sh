@@ -12,7 +12,7 @@ TAG=${1:-c2}; CFG=${2:-c2}; shift 2 || true
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-B="python3 $R/bench.py --config $CFG"
+B="python3 $R/bench.py --config $CFG --fs-frames 0"
 P="--no-spans --no-cpu-baseline --steps ${PSTEPS:-10} --warmup ${PWARM:-2}"  # c5: PSTEPS=1 PWARM=0
 echo "[prof] bench line"
 timeout -k 10 600 $B "$@" > $O/bench.json 2> $O/bench.err

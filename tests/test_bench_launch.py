@@ -104,7 +104,7 @@ def test_bench_forced_rccl_group():
     device_id=...), the device-tensor all_reduce of the timing and the
     dist.gather of the decision records into rank 0 all run through RCCL;
     rank 0 then recomputes its block and checks the gathered records."""
-    r = run_bench(["--config", "c2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"],
+    r = run_bench(["--config", "c2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--fs-frames", "4"],
                   {"VAME_FORCE_PG": "1"}, timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -114,6 +114,27 @@ def test_bench_forced_rccl_group():
     assert d["gather"]["backend"] == "nccl"
     assert d["gather"]["check"]["byte_identical"] is True and len(d["gather"]["check"]["pocs"]) >= 1
     assert d["n_gpus"] == 1 and d["scaling_form"] == "streams"
+    check_frame_shard(d, 1, "nccl")
+
+
+def check_frame_shard(d, world, backend):
+    """The `frame_shard` record: one 2160p sequence cut into
+    pair blocks over the ranks, the gather into rank 0 inside the timed span,
+    rank 0's recompute check byte-identical."""
+    fs = d["frame_shard"]
+    assert fs["backend"] == backend and fs["check"]["byte_identical"] is True
+    assert fs["pairs"] == sum(min(4, p) for p in range(1, fs["frames"] + 1))
+    assert fs["ms"] >= fs["kernel_ms"]["max"] >= fs["kernel_ms"]["min"] > 0
+    assert fs["rows"] == fs["pairs"] * 494700 and fs["rows_per_s"] > 0
+    assert fs["exchange_ms"] >= 0 and fs["gather_ms_max"] >= 0
+    # every rank's slab is padded to the largest block's words: compact records
+    # of 20 (2-CP) + 28 (3-CP) bytes per candidate CU (247,350 per CP mode at
+    # 2160p), from every rank but rank 0
+    per_pair = 247350 * (20 + 28)
+    if world == 1:
+        assert fs["bytes_into_rank0"] == 0
+    else:
+        assert fs["bytes_into_rank0"] == (world - 1) * -(-fs["pairs"] // world) * per_pair
 
 
 @pytest.mark.gpu
@@ -125,7 +146,8 @@ def test_bench_gpus2_launches_two_ranks(weak):
     it ran in, and the gathered records byte-identical to rank 0's recompute
     (both weak-scaling forms: a sequence per rank, pair blocks of one)."""
     r = run_bench(["--gpus", "2", "--config", "c2", "--steps", "3", "--warmup", "1",
-                   "--no-cpu-baseline", "--weak", weak], {"VAME_DIST_BACKEND": "gloo"}, timeout=280)
+                   "--no-cpu-baseline", "--weak", weak, "--fs-frames", "6" if weak == "streams" else "0"],
+                  {"VAME_DIST_BACKEND": "gloo"}, timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -139,6 +161,13 @@ def test_bench_gpus2_launches_two_ranks(weak):
     assert d["gather"]["check"]["cut_pocs"] == []  # sequence: POC 1-2 | POC 3, no cut
     assert d["config"]["parallelism"].endswith("(a sequence of its own per rank)" if weak == "streams"
                                                else "(pair_shard of one sequence)")
+    if weak == "streams":  # POC 1-6 = 18 pairs, 9 per rank: POC 4 cut between the ranks
+        check_frame_shard(d, 2, "gloo")
+        assert d["frame_shard"]["check"]["cut_pocs"] == [4]
+    else:
+        assert "frame_shard" not in d
+    g = d["gather"]  # pack and exchange timed apart
+    assert g["pack_ms"] >= 0 and g["exchange_ms"] >= 0 and g["bytes_into_rank0"] > 0
 
 
 @pytest.mark.gpu
@@ -159,7 +188,7 @@ def test_bench_under_torchrun():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port),
                         os.path.join(REPO, "bench.py"), "--gpus", "2", "--config", "c2", "--steps", "3",
-                        "--warmup", "1", "--no-cpu-baseline"], env=e, capture_output=True, text=True,
+                        "--warmup", "1", "--no-cpu-baseline", "--fs-frames", "0"], env=e, capture_output=True, text=True,
                        timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -134,11 +134,11 @@ def test_alignment_selection(engines, modes):
 REF_HARNESS = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle", "_ref", "ref_harness_hip")
 
 
-def run_reference(tmp_path, W, H, lam, ref, cur, tag):
+def run_reference(tmp_path, W, H, lam, ref, cur, tag, extra=0):
     """The reference kernels themselves (oracle/_ref: affine.cl compiled
     unmodified for gfx950, the host's four launches replayed by
-    ref_harness_hip) on one (POC, ref) pair, run twice (A/B).  Returns the two
-    runs' {PRED: (cost, cpmv[n, 6])}."""
+    ref_harness_hip, ExtraGradientIter = `extra`) on one (POC, ref) pair, run
+    twice (A/B).  Returns the two runs' {PRED: (cost, cpmv[n, 6])}."""
     d = os.path.dirname(REF_HARNESS)
     nctu = {(3840, 2160): 510, (1920, 1080): 135}[(W, H)]
     ref.tofile(tmp_path / f"{tag}_ref.u16")
@@ -147,7 +147,7 @@ def run_reference(tmp_path, W, H, lam, ref, cur, tag):
     for ab in ("A", "B"):
         out = tmp_path / f"{tag}_{ab}"
         (tmp_path / f"{tag}_jobs_{ab}.txt").write_text(
-            f"{W} {H} {lam!r} 0 {tmp_path / (tag + '_ref.u16')} {tmp_path / (tag + '_cur.u16')} {out}\n")
+            f"{W} {H} {lam!r} {extra} {tmp_path / (tag + '_ref.u16')} {tmp_path / (tag + '_cur.u16')} {out}\n")
         subprocess.run([REF_HARNESS, os.path.join(d, "affine_2cp.co"), os.path.join(d, "affine_3cp.co"),
                         str(tmp_path / f"{tag}_jobs_{ab}.txt")], check=True, timeout=300, capture_output=True)
         res = {}
@@ -159,7 +159,7 @@ def run_reference(tmp_path, W, H, lam, ref, cur, tag):
     return runs
 
 
-def check_vs_live_reference(runs, out, key_of, ref, cur, lam):
+def check_vs_live_reference(runs, out, key_of, ref, cur, lam, extra=0):
     """HIP results `out[key_of(PRED)]` vs the reference's two runs.  The
     reference hands gradients and equations between work-items through global
     memory behind only a local barrier (affine.cl:487-514, 715-738), so one of
@@ -170,7 +170,7 @@ def check_vs_live_reference(runs, out, key_of, ref, cur, lam):
     racy = [name for name in MODES if not (np.array_equal(runs[0][name][0], runs[1][name][0])
                                            and np.array_equal(runs[0][name][1], runs[1][name][1]))]
     if racy:
-        want = O.affine_me_pair(ref, cur, lam)
+        want = O.affine_me_pair(ref, cur, lam, extra)
         for name, key in MODES.items():
             hc, hp = host(out[key_of(name)])
             oc, op = want[key]
@@ -198,39 +198,47 @@ def test_live_reference_1080p(engines, tmp_path):
     check_vs_live_reference(runs, out, lambda name: (0, name), r[0], o[0], lam)
 
 
-# (W, H, QP, POC, refIdx) at the BASELINE configs' sizes:
-#   C4  3840x2160 POC 1 at the QP22 and QP37 lambdas (and their recon noise)
+# (W, H, QP, POC, refIdx, ExtraGradientIter) at the BASELINE configs' sizes
+# (VERDICT r3 item 2, r4 item 6):
+#   C4  3840x2160 POC 1 at the QP22 and QP37 lambdas (and their recon noise),
+#       POC 2 refIdx 1 at QP27
 #   C5  3840x2160 QP32 POC 239 refIdx 3: long-term reference POC 216, 23
 #       frames back -- the deepest motion of the sequence, many windows
 #       outside the staged tile (the mixed filter pass)
 #   C3  1920x1080 QP32 POC 26 refIdx 3: long-term reference POC 16
-LIVE_CASES = [(3840, 2160, 22, 1, 0), (3840, 2160, 37, 1, 0), (3840, 2160, 32, 239, 3),
-              (1920, 1080, 32, 26, 3)]
+#   C2  1920x1080 QP32 POC 2 refIdx 0 and 1: the benchmarked step's own pairs
+#       (bench.py's sequence, seed 0x5EED, lambda 70.34)
+#   ExtraGradientIter = 2 at 1920x1080 QP32 POC 1 (2-CP: 8 predictions per CU,
+#       3-CP: 7; affine.cl:172-177)
+LIVE_CASES = [(3840, 2160, 22, 1, 0, 0), (3840, 2160, 37, 1, 0, 0), (3840, 2160, 27, 2, 1, 0),
+              (3840, 2160, 32, 239, 3, 0), (1920, 1080, 32, 26, 3, 0), (1920, 1080, 32, 2, 0, 0),
+              (1920, 1080, 32, 2, 1, 0), (1920, 1080, 32, 1, 0, 2)]
 
 
 @pytest.mark.skipif(not os.path.exists(REF_HARNESS), reason="reference kernels not built")
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("W,H,qp,poc,refidx", LIVE_CASES,
-                         ids=[f"{w}x{h}_qp{q}_poc{p}_ref{k}" for w, h, q, p, k in LIVE_CASES])
-def test_live_reference_configs(engines, tmp_path, W, H, qp, poc, refidx):
+@pytest.mark.parametrize("W,H,qp,poc,refidx,extra", LIVE_CASES,
+                         ids=[f"{w}x{h}_qp{q}_poc{p}_ref{k}" + (f"_extra{x}" if x else "")
+                              for w, h, q, p, k, x in LIVE_CASES])
+def test_live_reference_configs(engines, tmp_path, W, H, qp, poc, refidx, extra):
     """The reference kernels vs the HIP batch path (vame_affine_me_batch, the
-    benchmarked entry point) on pairs of the C3 / C4 / C5 sequences, with the
-    reference's ring (main.cpp:591-707) and per-POC lambda (main.cpp:585):
+    benchmarked entry point) on pairs of the C2 / C3 / C4 / C5 sequences, with
+    the reference's ring (main.cpp:591-707) and per-POC lambda (main.cpp:585):
     all four PREDs, every cost and CPMV component, bit for bit."""
     from vame import synth
     from vame.hostlogic import lambda_for_poc, ref_list
     rp = ref_list(poc)[refidx]
     orig, recon = synth.synth_pocs(W, H, [poc], [rp], qp)
     lam = lambda_for_poc(qp, poc)
-    runs = run_reference(tmp_path, W, H, lam, recon[rp], orig[poc], f"p{poc}r{refidx}")
+    runs = run_reference(tmp_path, W, H, lam, recon[rp], orig[poc], f"p{poc}r{refidx}", extra)
     eng = engines(W, H)
     # the POC's whole ring in one batch, as the bench codes it; refIdx `refidx` is checked
     refs = ref_list(poc)
     others = synth.synth_pocs(W, H, [], [p for p in refs if p != rp], qp)[1]
     d_refs = [dev(recon[p]) if p == rp else dev(others[p]) for p in refs]
     job = (dev(orig[poc]), d_refs, lam, eng.alloc_poc(len(refs), 3))
-    eng.affine_me_batch([job], 3, 0)
-    check_vs_live_reference(runs, job[3], lambda name: (refidx, name), recon[rp], orig[poc], lam)
+    eng.affine_me_batch([job], 3, extra)
+    check_vs_live_reference(runs, job[3], lambda name: (refidx, name), recon[rp], orig[poc], lam, extra)
     # both packings of the 128-class CUs: this short launch ran the CTU items;
     # the long launches of the configs run affine_me_half (VAME_HALF128=1 here)
     from vame.engine import Engine
@@ -245,8 +253,8 @@ def test_live_reference_configs(engines, tmp_path, W, H, qp, poc, refidx):
             os.environ["VAME_HALF128"] = old
     try:
         job_h = (job[0], d_refs, lam, eng_half.alloc_poc(len(refs), 3))
-        eng_half.affine_me_batch([job_h], 3, 0)
-        check_vs_live_reference(runs, job_h[3], lambda name: (refidx, name), recon[rp], orig[poc], lam)
+        eng_half.affine_me_batch([job_h], 3, extra)
+        check_vs_live_reference(runs, job_h[3], lambda name: (refidx, name), recon[rp], orig[poc], lam, extra)
     finally:
         eng_half.close()
 
@@ -508,3 +516,67 @@ def test_block_order_variants(combos, order, monkeypatch):
         assert torch.equal(want[k][0], got[k][0]) and torch.equal(want[k][1], got[k][1]), k
     eng.close()
     base.close()
+
+
+PROBE = os.path.join(os.path.dirname(__file__), "native", "anyorder_probe")
+
+
+@pytest.mark.skipif(not os.path.exists(PROBE), reason="make probe")
+@pytest.mark.timeout(120)
+def test_event_after_anyorder_kernels_waits_for_all():
+    """a call's kernels after its first carry no AQL barrier bit
+    (hipExtAnyOrderLaunch), so its last packet may finish before its first.
+    Consumers ordering on an event recorded after the call (torch wait_stream,
+    an event + a copy on another stream) need the event's marker to wait for
+    every preceding packet.  The probe runs the structure with a 60 ms first
+    kernel and a tiny any-order one: the event (timing on and off) completes
+    only after the long kernel, and a copy on a second stream made to wait on
+    it sees every workgroup's done flag."""
+    import json
+    r = subprocess.run([PROBE], capture_output=True, text=True, timeout=100)
+    assert r.returncode in (0, 1), r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["all_ordered"] is True, d
+
+
+@pytest.mark.timeout(300)
+def test_call_results_ordered_by_event_on_another_stream(engines):
+    """ADVICE r4, on the engine itself: the default one-stream mode at
+    3840x2160 with 18 (POC, refIdx) pairs (>= 16: the 128-class CUs in
+    affine_me_ctu + affine_me_half after the quadrant kernel).  Result buffers
+    start as a sentinel; an event recorded right after affine_me_batch orders a
+    second stream, which copies every result to the host; the copies equal the
+    results read after a device-wide synchronize."""
+    from vame import synth
+    from vame.hostlogic import lambda_for_poc, ref_list
+    W, H, qp = 3840, 2160, 32
+    pocs = list(range(1, 7))  # 1 + 2 + 3 + 4 + 4 + 4 = 18 pairs
+    orig, recon = synth.synth_pocs(W, H, pocs, sorted({p for q in pocs for p in ref_list(q)}), qp)
+    eng = engines(W, H)
+    jobs = []
+    for poc in pocs:
+        out = eng.alloc_poc(len(ref_list(poc)), 3)
+        for c, p in out.values():
+            c.fill_(-7)
+            p.fill_(-7)
+        jobs.append((dev(orig[poc]), [dev(recon[p]) for p in ref_list(poc)], lambda_for_poc(qp, poc), out))
+    torch.cuda.synchronize()
+    eng.affine_me_batch(jobs, 3, 0)
+    ev = torch.cuda.Event()
+    ev.record()
+    side = torch.cuda.Stream()
+    side.wait_event(ev)
+    copies = []
+    with torch.cuda.stream(side):
+        for job in jobs:
+            for key, (c, p) in job[3].items():
+                hc = torch.empty(c.shape, dtype=c.dtype, pin_memory=True)
+                hp = torch.empty(p.shape, dtype=p.dtype, pin_memory=True)
+                hc.copy_(c, non_blocking=True)
+                hp.copy_(p, non_blocking=True)
+                copies.append((hc, hp, c, p))
+    side.synchronize()
+    torch.cuda.synchronize()
+    for hc, hp, c, p in copies:
+        assert torch.equal(hc, c.cpu()) and torch.equal(hp, p.cpu())
+        assert (hc != -7).all()

@@ -92,17 +92,23 @@ class ShardRun:
             self.eng.affine_me_batch(self.jobs, self.modes, 0)
 
     def slab(self) -> torch.Tensor:
+        """This rank's decision records packed into its compact slab (on the GPU)."""
         return shard.pack([j[3] for j in self.jobs], self.words, self.device, modes=self.modes)
 
-    def gather(self):
-        """The decision-record gather into rank 0: (slabs on rank 0 / None, bytes
-        moved into rank 0)."""
+    def exchange(self, slab: torch.Tensor):
+        """The exchange step alone: every rank's packed slab into rank 0 (RCCL;
+        under gloo, the CPU rehearsal of that path).  Returns (slabs on rank 0 /
+        None, bytes moved into rank 0)."""
         import torch.distributed as dist
-        slab = self.slab()
         if dist.is_available() and dist.is_initialized() and dist.get_backend() == "gloo":
             slab = slab.cpu()  # CPU rehearsal of the RCCL path
         slabs = shard.gather_to_root(slab, self.world, 0)
         return slabs, 4 * self.words * (self.world - 1)
+
+    def gather(self):
+        """The decision-record gather into rank 0 (pack + exchange): (slabs on
+        rank 0 / None, bytes moved into rank 0)."""
+        return self.exchange(self.slab())
 
     def verify_own(self) -> dict:
         """This rank's first and last block entry recomputed and compared with
