@@ -152,6 +152,11 @@ def test_launch_batches_and_cuts():
     batches = distrun.launch_batches(blocks)
     assert [e for b in batches for e in b] == blocks
     assert all(sum(len(r) for _, r in b) <= distrun.MAX_PAIRS for b in batches)
+    # a small first launch (the GPU starts once its frames are parsed), then full ones
+    small = distrun.launch_batches(blocks, 8)
+    assert [e for b in small for e in b] == blocks
+    assert sum(len(r) for _, r in small[0]) <= 8
+    assert all(sum(len(r) for _, r in b) <= distrun.MAX_PAIRS for b in small[1:])
     # the 6-POC sequence over 2 / 3 ranks cuts POC 4 / POC 5 between ranks
     for world, cut in ((2, [4]), (3, [5])):
         owners = {}
@@ -169,8 +174,8 @@ def test_one_rank_logs_byte_identical(seq):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("world", [2, 3])
 def test_gathered_logs_byte_identical(seq, world):
-    """Default path: records gathered into rank 0, which writes every POC."""
-    assert len(compare_dirs(run_ranks(seq, world, f"gather{world}"), seq / "expected")) == 40
+    """--gather-records: records gathered into rank 0, which writes every POC."""
+    assert len(compare_dirs(run_ranks(seq, world, f"gather{world}", ["--gather-records"]), seq / "expected")) == 40
 
 
 def self_gather_worker(rank, world, port, argv, table_path):
@@ -186,7 +191,8 @@ def test_one_rank_group_gathers_its_own_records(seq):
     out = seq / "selfgather"
     out.mkdir()
     argv = ["-f", str(SEQ["n"]), "-s", f"{SEQ['W']}x{SEQ['H']}", "-q", str(SEQ["qp"]),
-            "-o", str(seq / "orig.csv"), "-r", str(seq / "recon.csv"), "-l", str(out / "log")]
+            "-o", str(seq / "orig.csv"), "-r", str(seq / "recon.csv"), "-l", str(out / "log"),
+            "--gather-records"]
     from vame.launch import free_port
     mp.spawn(self_gather_worker, args=(1, free_port(), argv, str(seq / "table.pt")), nprocs=1, join=True)
     assert len(compare_dirs(out, seq / "expected")) == 40
@@ -241,7 +247,7 @@ def test_rank_only_part_files_are_replaced(seq):
 def test_shard_logs_byte_identical(seq, world):
     """--shard-logs: every rank writes its block, parts merged at their offsets;
     no part file is left behind."""
-    out = run_ranks(seq, world, f"shard{world}", ["--shard-logs"])
+    out = run_ranks(seq, world, f"shard{world}")  # the default path
     assert len(compare_dirs(out, seq / "expected")) == 40
 
 
@@ -302,7 +308,7 @@ def test_distrun_two_ranks_equals_cli(tmp_path, W, H, n):
     write_csv(str(tmp_path / "orig.csv"), orig)
     write_csv(str(tmp_path / "recon.csv"), recon)
     cli = run_cli(tmp_path, W, H, n, 32)
-    for name, extra in (("gather", ()), ("shard", ("--shard-logs",))):
+    for name, extra in (("gather", ("--gather-records",)), ("shard", ())):
         out, stdout = run_distrun_gpu(tmp_path, W, H, n, 32, name, ("--gpus", "2", *extra))
         assert len(compare_dirs(out, cli)) == 40, name
         assert "LOG_BYTES," in stdout and '"ranks": 2' in stdout
@@ -322,7 +328,7 @@ def test_distrun_forced_rccl_group_equals_cli(tmp_path):
     write_csv(str(tmp_path / "orig.csv"), orig)
     write_csv(str(tmp_path / "recon.csv"), recon)
     cli = run_cli(tmp_path, W, H, n, 32)
-    out, stdout = run_distrun_gpu(tmp_path, W, H, n, 32, "rccl1", (),
+    out, stdout = run_distrun_gpu(tmp_path, W, H, n, 32, "rccl1", ("--gather-records",),
                                   {"VAME_DIST_BACKEND": "nccl", "VAME_FORCE_PG": "1"})
     assert len(compare_dirs(out, cli)) == 40
     assert '"ranks": 1' in stdout and "LOG_GATHER_TIME," in stdout
@@ -395,6 +401,6 @@ def test_eight_ranks_cut_pocs_and_long_term_refs(tmp_path):
     a = distrun.parse_args(argv(one))
     distrun.run_rank(a, 1, 0, FakeEngine(416, 240), torch.device("cpu"))
     from vame.launch import free_port
-    for name, extra in (("gather8", ()), ("shard8", ("--shard-logs",))):
+    for name, extra in (("gather8", ("--gather-records",)), ("shard8", ())):
         mp.spawn(fake_worker, args=(8, free_port(), argv(tmp_path / name, *extra)), nprocs=8, join=True)
         assert len(compare_dirs(tmp_path / name, one)) == 20, name

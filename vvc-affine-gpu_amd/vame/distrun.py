@@ -5,24 +5,28 @@ main_aux_functions.h:387-525) -- with the POC loop cut into contiguous
 (POC, refIdx) pair blocks, one per rank (`shard.pair_shard`).
 
     python -m vame.distrun -f 240 -s 3840x2160 -q 32 -o orig.csv -r recon.csv \\
-        -l logs/out [--gpus N] [--shard-logs] [--modes all|2cp] [--ExtraGradientIter E]
+        -l logs/out [--gpus N] [--gather-records] [--modes all|2cp] [--ExtraGradientIter E]
 
-Every rank reads only the frames its block uses (`vame_read_frames_range`),
-codes its block in launches of up to 32 pairs (`vame_affine_me_batch`), and
-copies each launch's results to pinned host memory while the GPU runs the
+Every rank reads only the frames its block uses (`vame_read_frames_span`,
+each launch's frames parsed just before they go up, beside the kernels of
+the launches before), codes its block in launches of up to 32 pairs
+(`vame_affine_me_batch`; the first launch small, so the GPU starts early),
+and copies each launch's results to pinned host memory while the GPU runs the
 next one.  The logs are written in the reference's order by one of two paths:
 
-  default       the decision-log gather of the north star: rank 0 formats its
-                own block as it completes; every other rank packs its records
-                compactly on its GPU (`shard.pack`), and after the last launch
-                one gather (RCCL over xGMI) brings them to rank 0, which writes
-                them POC by POC.  Rank 0's CPU formats the whole log.
-  --shard-logs  every rank formats its own block as it completes -- rank 0
-                into the final files, rank k into host memory (a deferred
-                `vame_log_writer`) -- and at the end the ranks exchange their
-                byte counts per file (one all_reduce) and write their blocks
-                into the final files at their offsets, all ranks in parallel
-                (pwrite), so formatting and writing scale with the ranks.
+  default       the decision-log gather of byte counts: every rank formats
+                its own block as it completes -- rank 0 into the final files,
+                rank k into host memory (a deferred `vame_log_writer`) -- then
+                the ranks gather their byte counts per file (one all_reduce,
+                RCCL) and write their blocks into the final files at their
+                offsets, all ranks in parallel (pwrite), so formatting and
+                writing scale with the ranks.  (`--shard-logs` names this path
+                too.)
+  --gather-records  the records themselves to rank 0: every other rank packs
+                its records compactly on its GPU (`shard.pack`), and after the
+                last launch one gather (RCCL over xGMI) brings them to rank 0,
+                which formats and writes them POC by POC (rank 0's CPU formats
+                the whole log; for file systems the ranks do not share).
 
 Blocks are contiguous in coding order, and a POC cut between two ranks is cut
 at a refIdx boundary (refIdx is the outer loop of every file's rows), so both
@@ -63,7 +67,10 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--ExtraGradientIter", dest="extra", type=int, default=0)
     ap.add_argument("--modes", choices=("all", "2cp"), default="all")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--shard-logs", action="store_true")
+    ap.add_argument("--gather-records", action="store_true",
+                    help="gather the decision records into rank 0, which formats the whole log")
+    ap.add_argument("--shard-logs", action="store_true",
+                    help="every rank formats and places its own block (the default)")
     ap.add_argument("--rank-only", type=int, default=None, metavar="K",
                     help="run only rank K's share of a --gpus N job, alone on GPU 0 (no collective; "
                          "its logs stay part files): prices one rank of an N-GPU node on one GPU")
@@ -78,6 +85,9 @@ def parse_args(argv=None) -> argparse.Namespace:
         ap.error("frames and gpus must be >= 1, ExtraGradientIter in 0..64")
     if a.rank_only is not None and not 0 <= a.rank_only < a.gpus:
         ap.error("--rank-only K needs 0 <= K < --gpus")
+    if a.gather_records and a.shard_logs:
+        ap.error("--gather-records and --shard-logs are two log paths: pick one")
+    a.shard_logs = not a.gather_records
     if shard.sequence_pairs(a.frames) < a.gpus:  # every rank codes at least one pair
         ap.error(f"--gpus {a.gpus} needs at least as many (POC, refIdx) pairs "
                  f"({shard.sequence_pairs(a.frames)} in {a.frames} frames)")
@@ -89,11 +99,13 @@ def part_prefix(prefix: str, rank: int) -> str:
     return f"{prefix}.part{rank}"
 
 
-def launch_batches(blocks):
-    """The block's entries in launches of at most MAX_PAIRS pairs (entries whole)."""
+def launch_batches(blocks, first: int = MAX_PAIRS):
+    """The block's entries in launches of at most MAX_PAIRS pairs (entries
+    whole); the first launch holds at most `first` pairs (the GPU starts once
+    its few frames are parsed, while the rest are parsed behind it)."""
     out, cur, n = [], [], 0
     for poc, refs in blocks:
-        if cur and n + len(refs) > MAX_PAIRS:
+        if cur and n + len(refs) > (first if not out else MAX_PAIRS):
             out.append(cur)
             cur, n = [], 0
         cur.append((poc, refs))
@@ -144,18 +156,42 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
     # together: rank r counts the newlines of chunks r, r + N, ... and one
     # all_reduce shares the counts; each rank then parses only the chunks that
     # hold its frames.
+    # With the line index, each launch's frames are parsed just before they go
+    # up, in the uploader thread (below), so the GPU starts after the first
+    # launch's frames only and the rest of the ingest runs beside the kernels
+    # (the reference reads every frame first, main.cpp:293-330); without it (a
+    # one-rank run, raw frames) the block's frames are read at once, here.
     t = time.perf_counter()
     idx = {path: line_index(path, world, rank, dist, T) for path in (a.orig, a.recon)}
+    T["index_s"] = time.perf_counter() - t - T.get("index_others_s", 0.0)
     d_orig, d_recon = {}, {}
-    if blocks:
-        pocs = [p for p, _ in blocks]
-        need = sorted({ref_list(p)[r] for p, refs in blocks for r in refs})
+    orig, recon = {}, {}  # host frames by POC
+    pocs = [p for p, _ in blocks]
+    need = sorted({ref_list(p)[r] for p, refs in blocks for r in refs})
+    parse_s = [0.0]
 
-        def read(path, first, n):
+    def read_into(store, path, frames):
+        """Parse `frames` (POC numbers, 0-based frame index in the file) of
+        `path` into `store`, one contiguous run of frames per read."""
+        frames = sorted(f for f in set(frames) if f not in store)
+        t0 = time.perf_counter()
+        k = 0
+        while k < len(frames):
+            e = k
+            while e + 1 < len(frames) and frames[e + 1] == frames[e] + 1:
+                e += 1
+            first, n = frames[k], frames[e] - frames[k] + 1
             span = None if idx[path] is None else logs.line_span(*idx[path], first * H, (first + n) * H)
-            return logs.read_frames(path, W, H, n, first=first, span=span)
-        orig = read(a.orig, pocs[0] - 1, pocs[-1] - pocs[0] + 1)
-        recon = read(a.recon, need[0], need[-1] - need[0] + 1)
+            got = logs.read_frames(path, W, H, n, first=first, span=span)
+            for i in range(n):
+                store[first + i] = got[i]
+            k = e + 1
+        parse_s[0] += time.perf_counter() - t0
+
+    overlap = blocks and idx[a.orig] is not None and idx[a.recon] is not None
+    if blocks and not overlap:
+        read_into(orig, a.orig, [p - 1 for p in pocs])
+        read_into(recon, a.recon, need)
     T["read_csv_s"] = time.perf_counter() - t - T.get("index_others_s", 0.0)
 
     # frames go to the device launch by launch, ahead of the kernels, from a
@@ -167,7 +203,8 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
     # hardware queues, and a copy stream sharing the compute stream's queue
     # puts each launch's result download in front of the next launch (the
     # vame CLI measured 5.1 ms of idle GPU per 4-POC 4K launch that way).
-    batches = list(launch_batches(blocks))
+    batches = list(launch_batches(blocks, int(os.environ.get("VAME_FIRST_LAUNCH_PAIRS", "8")) if overlap
+                                  else MAX_PAIRS))
     compute = torch.cuda.current_stream(device) if cuda else None
     prio = int(os.environ.get("VAME_COPY_PRIO", "-1"))
     upstream = torch.cuda.Stream(device, priority=prio) if cuda else None
@@ -190,11 +227,20 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
                 for b, batch in enumerate(batches):
                     if up_stop.is_set():
                         break
+                    if overlap:  # this launch's frames, parsed now
+                        read_into(orig, a.orig, [p - 1 for p, _ in batch])
+                        read_into(recon, a.recon, [ref_list(p)[r] for p, refs in batch for r in refs])
+                        if b == 0:
+                            T["first_frames_s"] = time.perf_counter() - t_start
                     for poc, refs in batch:
                         rl = ref_list(poc)
-                        frame(d_orig, poc, orig[poc - pocs[0]])
+                        frame(d_orig, poc, orig[poc - 1])
                         for r in refs:
-                            frame(d_recon, rl[r], recon[rl[r] - need[0]])
+                            frame(d_recon, rl[r], recon[rl[r]])
+                    if overlap:  # host frames no later launch reads
+                        last = max(p for p, _ in batch)
+                        for q in [q for q in orig if q + 1 <= last]:
+                            del orig[q]
                     if cuda:
                         up_ev[b] = torch.cuda.Event()
                         up_ev[b].record(upstream)
@@ -312,6 +358,9 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
     up_th.join()
     if err:
         raise err[0]
+    if overlap:  # parsed in the uploader thread, beside the launches
+        T["read_csv_s"] += parse_s[0]
+        T["read_csv_overlapped"] = True
     if slab_parts:
         shard.check_flag(pack_bad)
     if cuda:
