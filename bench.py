@@ -215,17 +215,18 @@ def main():
     if not step_ms:  # fewer timed steps than one sample period
         step_ms = [elapsed * 1e3 / max(args.steps, 1)]
     quad_ms, quad_n = eng.get_timing(0)
-    # the 128-class kernels (128x128 CUs: affine_me_ctu, class 1; 128x64 /
-    # 64x128 CUs: affine_me_half, class 2), timed in the sampled timed steps
-    # with VAME_BENCH_KTIMING=1, else on extra untimed steps after them
-    big_t = {k: eng.get_timing(k) for k in (1, 2)}
+    # the 128-class kernels (CTU items: affine_me_ctu, class 1; 128x64 /
+    # 64x128 CUs: affine_me_half, class 2; 128x128 CUs: affine_me_ctu2, class
+    # 3), timed in the sampled timed steps with VAME_BENCH_KTIMING=1, else on
+    # extra untimed steps after them
+    big_t = {k: eng.get_timing(k) for k in (1, 2, 3)}
     big_on = "the sampled timed steps"
     if ktiming != 1:
         big_steps = min(args.steps, 20)
         eng.set_timing(True)
         for _ in range(big_steps):
             run.step()
-        big_t = {k: eng.get_timing(k) for k in (1, 2)}
+        big_t = {k: eng.get_timing(k) for k in (1, 2, 3)}
         eng.get_timing(0)
         big_on = f"{big_steps} untimed steps after the timed ones"
     eng.set_timing(False)
@@ -285,15 +286,18 @@ def main():
     quad_avg = quad_ms / quad_n if quad_n else 0.0
     roof_q = kernel_roof(quad_avg, per_launch("bytes_quad"), prof.get("kernels", {}).get("affine_me_quad"),
                          pc.get("executed_pred_frac_quad"))
-    # per 128-class kernel: with affine_me_half launches (a launch of >= 16
-    # pairs, the engine's default) the CTU items hold only the 128x128 CUs;
-    # otherwise all 128-class CUs (a mix of both packings in one step leaves
-    # the CTU kernel's bytes unattributed)
+    # per 128-class kernel, the algorithmic bytes it carries: the 128x128 CUs
+    # run in affine_me_ctu2 (the default) or in CTU items; the 128x64 / 64x128
+    # CUs in affine_me_half (launches of >= 16 pairs) or in CTU items (shorter
+    # launches).  A step mixing both packings leaves the CTU kernel's bytes
+    # unattributed.
+    ctu2 = big_t[3][1] > 0
     split = big_t[2][1] > 0
-    mixed = split and big_t[2][1] != big_t[1][1]
+    mixed = split and (big_t[2][1] != big_t[1][1] if not ctu2 else big_t[1][1] > 0)
+    ctu_key = ("bytes_half" if ctu2 else "bytes_ctu") if split or ctu2 else "bytes_big"
     big_kernels = {}
-    for k, name, key in ((1, "affine_me_ctu", "bytes_ctu" if split else "bytes_big"),
-                         (2, "affine_me_half", "bytes_half")):
+    for k, name, key in ((1, "affine_me_ctu", ctu_key), (2, "affine_me_half", "bytes_half"),
+                         (3, "affine_me_ctu2", "bytes_ctu")):
         ms, n = big_t[k]
         if n == 0 or (mixed and k == 1):
             continue

@@ -66,7 +66,7 @@ typedef struct {
  * Tuning knobs read here (results are bit-identical under every setting; the
  * defaults are the measured best on MI355X): work packing
  * VAME_TASKS (wave tasks per autonomous quadrant item, 1..16, default 16),
- * VAME_CLAIM, VAME_CHAIN, VAME_MIX (default 1 each), VAME_HALF128,
+ * VAME_CLAIM, VAME_CHAIN, VAME_MIX (default 1 each), VAME_HALF128, VAME_CTU2,
  * VAME_HALF_MIN_PAIRS; launch structure VAME_STREAMS, VAME_QUAD_FIRST,
  * VAME_GRAPH, VAME_JOIN_EACH; block order VAME_ITEM_ORDER, VAME_XCD_ORDER, VAME_GROUP_COMBOS,
  * VAME_GROUP_COMBOS_BIG. */
@@ -105,6 +105,19 @@ typedef struct {
 int vame_affine_me_batch(vame_ctx* ctx, const vame_poc_job* jobs, int njobs, int mode_mask,
                          int extra_grad_iter, void* stream);
 
+/* The compact wire form of the jobs' decision records, for the frame-shard
+ * gather into rank 0 (vame/shard.py pack() is its
+ * specification): for each job in order, refIdx 0..nrefs-1, each PRED of
+ * vame_pred_mask(mode_mask) in PRED order: the nCtus*{201|284} costs as
+ * int32, then the records' CPMV components (LT, RT, and LB for 3-CP: 4 or 6
+ * int32 each).  `slab` (device, `words` int32) is zero-filled past the
+ * records; `*bad` (device int32) is OR-ed with 1 when a record does not fit
+ * the form (cost outside [0, 2^31), 2-CP LB != 0).  One kernel on `stream`;
+ * the jobs' cur / refs / lambda are not read.  VAME_E_INVALID when the records
+ * exceed `words`. */
+int vame_pack_records(vame_ctx* ctx, const vame_poc_job* jobs, int njobs, int mode_mask, int32_t* slab,
+                      long long words, int32_t* bad, void* stream);
+
 /* PROF (prediction refinement with optical flow).  The reference carries the
  * code but hard-disables it (`int enablePROF=0`, affine.cl:168 / :1132;
  * aux_functions.cl:215-605, :1096-1239); enable != 0 turns it on for the
@@ -115,9 +128,11 @@ int vame_set_prof(vame_ctx* ctx, int enable);
 /* Device-side kernel timing (the reference's per-PRED kernelExecutionTime,
  * main.cpp:856-866): when enabled, every kernel launch carries hipEvents in its
  * own dispatch on the stream it runs on.  kernel_class 0 = quadrant work items
- * (affine_me_quad), 1 = CTU items (affine_me_ctu: the 128x128 CUs, and in
- * launches of fewer than VAME_HALF_MIN_PAIRS pairs -- or with VAME_HALF128=0 --
- * the 128x64 / 64x128 CUs too), 2 = single 128x64 / 64x128 CUs (affine_me_half).
+ * (affine_me_quad); 1 = CTU items (affine_me_ctu: every 128-class CU in launches
+ * of fewer than VAME_HALF_MIN_PAIRS pairs); 2 = single 128x64 / 64x128 CUs
+ * (affine_me_half) and 3 = single 128x128 CUs (affine_me_ctu2), both in
+ * launches of at least VAME_HALF_MIN_PAIRS pairs (VAME_HALF128 / VAME_CTU2
+ * select the other packings).
  * enable = 2 times the quadrant kernel only (its dispatches carry the events;
  * the 128-class launches run untimed).  vame_get_timing waits for the recorded
  * launches and returns their summed duration and count since the last reset.

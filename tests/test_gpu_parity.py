@@ -438,11 +438,14 @@ def test_property_translation_1080p(engines, d):
                                  {"VAME_GRAPH": "1"}, {"VAME_GRAPH": "1", "VAME_HALF128": "1"},
                                  {"VAME_GRAPH": "1", "VAME_STREAMS": "2"}, {"VAME_MIX": "0"},
                                  {"VAME_TASKS": "8"}, {"VAME_TASKS": "4", "VAME_CHAIN": "0", "VAME_MIX": "0"},
-                                 {"VAME_TASKS": "1"}, {"VAME_CLAIM": "0"}, {"VAME_ITEM_ORDER": "0"}],
+                                 {"VAME_TASKS": "1"}, {"VAME_CLAIM": "0"}, {"VAME_ITEM_ORDER": "0"},
+                                 {"VAME_CTU2": "2"}, {"VAME_CTU2": "0", "VAME_HALF128": "1"},
+                                 {"VAME_GRAPH": "1", "VAME_CTU2": "2"}],
                          ids=["half512_packing", "ctu1024_packing", "two_streams", "two_streams_half512",
                               "ctu_first", "graph", "graph_half512", "graph_two_streams", "aligns_unmixed",
                               "items_of_8", "items_of_4_unchained_unmixed", "items_of_1_task",
-                              "static_tasks", "items_by_quadrant"])
+                              "static_tasks", "items_by_quadrant", "ctu2_in_short_launches",
+                              "ctu1024_128x128_half512", "graph_ctu2_in_short_launches"])
 def test_launch_structure_variants(env, monkeypatch):
     """The engine's launch-structure knobs (read at vame_create) change only
     where the work runs: VAME_HALF128=1 gives every 128x64 / 64x128 CU a
@@ -452,6 +455,9 @@ def test_launch_structure_variants(env, monkeypatch):
     quadrant kernel instead of issuing every kernel of a call on the caller's
     stream (all but the first without the AQL barrier bit, the default);
     VAME_QUAD_FIRST=0 issues the 128-class kernels before the quadrant kernel;
+    VAME_CTU2=2 runs the 128x128 CUs in affine_me_ctu2 (512 threads, two
+    stacked sub-blocks per lane; by default only in launches of >= 16 pairs)
+    and 0 never;
     VAME_TASKS=8 / 4 / 1 packs 8 / 4 / 1 wave tasks per autonomous quadrant
     item (default 16 over the one staged tile, each wave claiming the next
     task as it finishes; VAME_CLAIM=0: wave w runs tasks w, w + 4, ...),
@@ -580,3 +586,36 @@ def test_call_results_ordered_by_event_on_another_stream(engines):
     for hc, hp, c, p in copies:
         assert torch.equal(hc, c.cpu()) and torch.equal(hp, p.cpu())
         assert (hc != -7).all()
+
+
+@pytest.mark.parametrize("modes", [1, 3, 3 | 8])
+def test_pack_records_equals_shard_pack(engines, modes):
+    """vame_pack_records (one kernel) == shard.pack, its specification, word
+    for word, zero-padded past the records; a record the compact form cannot
+    hold (a cost of 2^31, a 2-CP LB) sets the flag."""
+    from vame import shard
+    eng = engines(416, 240)
+    g = torch.Generator(device="cuda").manual_seed(modes)
+    res = []
+    for nrefs in (1, 3):
+        out = eng.alloc_poc(nrefs, modes)
+        for (r, name), (c, p) in out.items():
+            c.copy_(torch.randint(0, 2**31 - 1, c.shape, device="cuda", generator=g))
+            p.copy_(torch.randint(-2**17, 2**17, p.shape, device="cuda", generator=g, dtype=torch.int32))
+            if name.endswith("2CP"):
+                p[:, 5:] = 0
+        res.append(out)
+    words = shard.slab_words([(1, modes, (eng.n_cus(0), eng.n_cus(1))), (3, modes, (eng.n_cus(0), eng.n_cus(1)))])
+    bad = torch.zeros((), dtype=torch.int32, device="cuda")
+    got = eng.pack_records(res, modes, words + 100, bad)
+    want = shard.pack(res, words + 100, modes=modes)
+    assert torch.equal(got, want) and int(bad) == 0
+    key = next(k for k in res[1] if k[1].endswith("2CP"))
+    res[1][key][1][7, 6] = 4  # LB of a 2-CP record
+    eng.pack_records(res, modes, None, bad)
+    assert int(bad) == 1
+    res[1][key][1][7, 6] = 0
+    res[0][next(iter(res[0]))][0][3] = 2**31
+    bad.zero_()
+    eng.pack_records(res, modes, None, bad)
+    assert int(bad) == 1

@@ -42,8 +42,19 @@ struct vame_ctx {
   Item* dQuad = nullptr;
   Item* dBig3 = nullptr;
   Item* dBig1 = nullptr;
+  Item* dBig2 = nullptr;  // dBig3 without the 128x128 item (that one runs in affine_me_ctu2)
   Item* dHalf = nullptr;
-  int nQuadFull = 0, nQuadHalf = 0, nQuadBoth = 0, nBig3 = 0, nBig1 = 0, nHalf = 0;
+  int nQuadFull = 0, nQuadHalf = 0, nQuadBoth = 0, nBig3 = 0, nBig1 = 0, nBig2 = 0, nHalf = 0;
+  // VAME_CTU2: where the 128x128 CUs run -- 1 (default): in affine_me_ctu2
+  // (512 threads, two stacked sub-blocks per lane, two workgroups per CU) in
+  // the launches that use affine_me_half (>= halfMinPairs pairs), in the CTU
+  // items in shorter ones (the 3-pair c2 step: there the 128-class work is
+  // under two rounds of workgroups and a kernel more only adds a tail); 2:
+  // always in affine_me_ctu2; 0: always in CTU items.  affine_me_ctu2's 3-CP
+  // seed-reuse sums live in bestS (kMaxPairs x nCtus x 5 x 1024 int32,
+  // allocated on first use)
+  int ctu2 = 1;
+  int32_t* bestS = nullptr;
   // which packing a launch uses (VAME_HALF128): 0 always dBig3, 1 always
   // dBig1 + dHalf, 2 (default) dBig1 + dHalf for launches of at least
   // halfMinPairs (POC, refIdx) pairs (VAME_HALF_MIN_PAIRS, default 16), dBig3
@@ -62,7 +73,8 @@ struct vame_ctx {
   hipStream_t side = nullptr;   // second stream: 128-class items run beside the quadrant items
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   // optional per-kernel timing: (start, end) event pairs per kernel class
-  // (0 quadrant, 1 128x128 CTU, 2 128x64 / 64x128 CUs)
+  // (0 quadrant, 1 CTU items, 2 128x64 / 64x128 CUs, 3 128x128 CUs in
+  // affine_me_ctu2)
   int timing = 0;
   // PROF on (vame_set_prof): the *_prof kernels
   bool prof = false;
@@ -86,9 +98,46 @@ struct vame_ctx {
     hipGraphExec_t exec;
   };
   std::vector<GraphEntry> graphs;  // most recent last, at most kMaxGraphs
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[3];
-  size_t evUsed[3] = {0, 0, 0};
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[4];
+  size_t evUsed[4] = {0, 0, 0, 0};
+  // vame_pack_records: the segment table of the last pack (host copy kept
+  // until the next call) and its device copy
+  std::vector<struct PackSeg> packSegs;
+  struct PackSeg* dPackSegs = nullptr;
+  size_t dPackCap = 0;
+  hipEvent_t packEv = nullptr;  // the last table upload (the host table is rewritten after it)
 };
+
+// One segment of a record pack: the n records of one (POC, refIdx, PRED),
+// costs to slab[off .. off + n), CPMV components after them.
+struct PackSeg {
+  const int64_t* cost;
+  const int32_t* cpmv;  // vame_cpmvs, 7 int32 per record
+  long long off;
+  int n, ncp;
+};
+
+// Compact wire form (shard.pack's specification): thread i of segment
+// blockIdx.y moves record i -- its cost as int32, its 2 * ncp CPMV components
+// -- and flags a record the form cannot hold (cost outside [0, 2^31), a 2-CP
+// LB other than (0, 0)).
+__global__ __launch_bounds__(256) void pack_records_kernel(const PackSeg* segs, int32_t* slab, int32_t* bad) {
+  const PackSeg sg = segs[blockIdx.y];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= sg.n) return;
+  const long long c = sg.cost[i];
+  const int32_t* r = sg.cpmv + (size_t)i * 7;
+  int flag = (c < 0 || c >= (1ll << 31)) ? 1 : 0;
+  slab[sg.off + i] = (int32_t)c;
+  int32_t* d = slab + sg.off + sg.n + (size_t)i * 2 * sg.ncp;
+  if (sg.ncp == 2) {
+    d[0] = r[1]; d[1] = r[2]; d[2] = r[3]; d[3] = r[4];
+    flag |= (r[5] | r[6]) != 0;
+  } else {
+    d[0] = r[1]; d[1] = r[2]; d[2] = r[3]; d[3] = r[4]; d[4] = r[5]; d[5] = r[6];
+  }
+  if (__builtin_amdgcn_ballot_w64(flag != 0) && flag) atomicOr(bad, 1);
+}
 
 namespace {
 
@@ -437,7 +486,10 @@ std::vector<int32_t> build_order(int nCtus, int cols, int groupCombos, int xcdOr
 using KernelFn = void (*)(KParams);
 template <int KIND>
 KernelFn kernel_for(bool prof, int mode) {
-  if constexpr (KIND == kKindCtu) {
+  if constexpr (KIND == kKindCtu2) {
+    (void)prof;  // PROF runs the 128x128 CUs in affine_me_ctu_prof (launch_direct)
+    return mode == 1 ? affine_me_ctu2<1> : mode == 2 ? affine_me_ctu2<2> : affine_me_ctu2<3>;
+  } else if constexpr (KIND == kKindCtu) {
     if (prof) return mode == 1 ? affine_me_ctu_prof<1> : mode == 2 ? affine_me_ctu_prof<2> : affine_me_ctu_prof<3>;
     return mode == 1 ? affine_me_ctu<1> : mode == 2 ? affine_me_ctu<2> : affine_me_ctu<3>;
   } else if constexpr (KIND == kKindHalf) {
@@ -495,8 +547,24 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
   };
   auto big = [&](const KParams& kp) -> int {
     KParams kb = kp;
-    kb.items = use_half(kp) ? c->dBig1 : c->dBig3;
-    kb.nItems = use_half(kp) ? c->nBig1 : c->nBig3;
+    const bool ctu2 = !c->prof && (c->ctu2 == 2 || (c->ctu2 == 1 && use_half(kp)));
+    if (ctu2) {  // the 128x128 CUs in affine_me_ctu2, the rest (short launches) in CTU items
+      kb.items = c->dBig1;
+      kb.nItems = c->nBig1;
+      kb.bestS = c->bestS;
+      const unsigned grid = block_grid(c, 1, kb);
+      hipEvent_t t0, t1;
+      VAME_TRY(time_events(c, 3, t0, t1));
+      VAME_HIP(launch_kernel(kernel_for<kKindCtu2>(false, mode), grid, Cfg<kKindCtu2>::THREADS, sBig, t0, t1,
+                             order_flag(), kb, capture));
+      if (use_half(kp)) return VAME_OK;
+      kb = kp;
+      kb.items = c->dBig2;
+      kb.nItems = c->nBig2;
+    } else {
+      kb.items = use_half(kp) ? c->dBig1 : c->dBig3;
+      kb.nItems = use_half(kp) ? c->nBig1 : c->nBig3;
+    }
     const unsigned grid = block_grid(c, 1, kb);
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 1, t0, t1));
@@ -562,6 +630,10 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
 
 int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool quadHalf, bool bigItems,
            hipStream_t stream) {
+  if (c->ctu2 && !c->bestS && bigItems && !kps.empty() && kps[0].run2 && kps[0].run3) {
+    // affine_me_ctu2's 3-CP seed-reuse sums: 5 x 1024 int32 per (pair, CTU) of a launch
+    VAME_HIP(hipMalloc(&c->bestS, (size_t)kMaxPairs * c->nCtus * 5 * Cfg<kKindCtu2>::NSB * sizeof(int32_t)));
+  }
   if (!c->useGraph || c->timing || kps.empty()) return launch_direct(c, kps, quadFull, quadHalf, bigItems, stream, false);
   // the call's identity: its kernel arguments and launch selection
   std::vector<unsigned char> key(kps.size() * sizeof(KParams) + 4);
@@ -651,9 +723,11 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (device < 0 || device >= ndev) return VAME_E_INVALID;
   DeviceGuard guard(device);
   VAME_HIP(guard.err);
-  std::vector<Item> big3, big1, hf, qf, qh, qb, unused;
+  std::vector<Item> big3, big1, big2, hf, qf, qh, qb, unused;
   const int tasks = tasks_per_item();
   build_templates(big3, unused, qf, qh, qb, false, tasks, chain_coop(), mix_aligns());
+  for (const Item& it : big3)  // the CTU items without the 128x128 one
+    if (it.cu[0].lw != it.cu[0].lh) big2.push_back(it);
   qf.clear();
   qh.clear();
   qb.clear();
@@ -666,6 +740,8 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   c->ctusPerRow = (width + kCtu - 1) / kCtu;  // T8: integer ceil
   c->nBig3 = (int)big3.size();
   c->nBig1 = (int)big1.size();
+  c->nBig2 = (int)big2.size();
+  c->ctu2 = std::min(2, std::max(0, env_int("VAME_CTU2", 1)));
   c->nHalf = (int)hf.size();
   c->halfMode = std::min(2, std::max(0, env_int("VAME_HALF128", 2)));
   c->halfMinPairs = std::max(1, env_int("VAME_HALF_MIN_PAIRS", 16));
@@ -693,6 +769,8 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   }
   if (e == hipSuccess) e = hipMalloc(&c->dBig3, big3.size() * sizeof(Item));
   if (e == hipSuccess) e = hipMalloc(&c->dBig1, big1.size() * sizeof(Item));
+  if (e == hipSuccess) e = hipMalloc(&c->dBig2, big2.size() * sizeof(Item));
+  if (e == hipSuccess) e = hipMemcpy(c->dBig2, big2.data(), big2.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->dQuad, quad.data(), quad.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->dBig3, big3.data(), big3.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->dBig1, big1.data(), big1.size() * sizeof(Item), hipMemcpyHostToDevice);
@@ -718,6 +796,8 @@ void vame_destroy(vame_ctx* c) {
   if (c->dQuad) (void)hipFree(c->dQuad);
   if (c->dBig3) (void)hipFree(c->dBig3);
   if (c->dBig1) (void)hipFree(c->dBig1);
+  if (c->dBig2) (void)hipFree(c->dBig2);
+  if (c->bestS) (void)hipFree(c->bestS);
   if (c->dHalf) (void)hipFree(c->dHalf);
   for (int k = 0; k < 2; k++)
     if (c->dOrder[k]) (void)hipFree(c->dOrder[k]);
@@ -726,7 +806,9 @@ void vame_destroy(vame_ctx* c) {
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->evFork) (void)hipEventDestroy(c->evFork);
   if (c->evJoin) (void)hipEventDestroy(c->evJoin);
-  for (int k = 0; k < 3; k++)
+  if (c->dPackSegs) (void)hipFree(c->dPackSegs);
+  if (c->packEv) (void)hipEventDestroy(c->packEv);
+  for (int k = 0; k < 4; k++)
     for (auto& e : c->ev[k]) {
       (void)hipEventDestroy(e.first);
       (void)hipEventDestroy(e.second);
@@ -853,6 +935,57 @@ int vame_affine_me_poc(vame_ctx* c, const uint16_t* cur, const uint16_t* const* 
   return vame_affine_me_batch(c, &job, 1, mode_mask, extra, stream);
 }
 
+int vame_pack_records(vame_ctx* c, const vame_poc_job* jobs, int njobs, int mode_mask, int32_t* slab,
+                      long long words, int32_t* bad, void* stream) {
+  if (!c || !jobs || njobs < 0 || !slab || !bad || words < 0) return VAME_E_INVALID;
+  if (!(mode_mask & VAME_MODE_2CP) || (mode_mask & ~15)) return VAME_E_INVALID;
+  const int preds = vame_pred_mask(mode_mask);
+  DeviceGuard guard(c->device);
+  VAME_HIP(guard.err);
+  if (c->packEv) VAME_HIP(hipEventSynchronize(c->packEv));  // the previous upload read the table
+  std::vector<PackSeg>& segs = c->packSegs;
+  segs.clear();
+  long long off = 0;
+  int maxn = 0;
+  for (int j = 0; j < njobs; j++) {
+    const vame_poc_job& jb = jobs[j];
+    if (!jb.out || jb.nrefs < 1 || jb.nrefs > 4) return VAME_E_INVALID;
+    for (int r = 0; r < jb.nrefs; r++)
+      for (int m = 0; m < 4; m++) {
+        if (!((preds >> m) & 1)) continue;
+        if (!jb.out->cost[r][m] || !jb.out->cpmvs[r][m]) return VAME_E_INVALID;
+        PackSeg sg;
+        sg.cost = jb.out->cost[r][m];
+        sg.cpmv = reinterpret_cast<const int32_t*>(jb.out->cpmvs[r][m]);
+        sg.n = c->nCtus * ((m >> 1) ? kHalfCusPerCtu : kFullCusPerCtu);
+        sg.ncp = (m & 1) ? 3 : 2;
+        sg.off = off;
+        off += (long long)sg.n * (1 + 2 * sg.ncp);
+        maxn = std::max(maxn, sg.n);
+        segs.push_back(sg);
+      }
+  }
+  if (off > words) return VAME_E_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  if (!c->packEv) VAME_HIP(hipEventCreateWithFlags(&c->packEv, hipEventDisableTiming));
+  if (segs.size() > c->dPackCap) {
+    if (c->dPackSegs) VAME_HIP(hipFree(c->dPackSegs));
+    c->dPackSegs = nullptr;
+    c->dPackCap = 0;
+    VAME_HIP(hipMalloc(&c->dPackSegs, segs.size() * sizeof(PackSeg)));
+    c->dPackCap = segs.size();
+  }
+  if (!segs.empty()) {
+    VAME_HIP(hipMemcpyAsync(c->dPackSegs, segs.data(), segs.size() * sizeof(PackSeg), hipMemcpyHostToDevice, s));
+    VAME_HIP(hipEventRecord(c->packEv, s));
+    hipLaunchKernelGGL(pack_records_kernel, dim3((maxn + 255) / 256, (unsigned)segs.size()), dim3(256), 0, s,
+                       c->dPackSegs, slab, bad);
+    VAME_HIP(hipGetLastError());
+  }
+  if (words > off) VAME_HIP(hipMemsetAsync(slab + off, 0, (size_t)(words - off) * sizeof(int32_t), s));
+  return VAME_OK;
+}
+
 int vame_set_prof(vame_ctx* c, int enable) {
   if (!c) return VAME_E_INVALID;
   c->prof = enable != 0;
@@ -866,13 +999,13 @@ int vame_set_timing(vame_ctx* c, int enable) {
   // a sample of its steps toggles timing between them)
   const bool keep = (enable & VAME_TIMING_KEEP) != 0;
   enable &= ~VAME_TIMING_KEEP;
-  c->timing = enable == 2 ? 1 : enable != 0 ? 7 : 0;
-  if (!keep) c->evUsed[0] = c->evUsed[1] = c->evUsed[2] = 0;
+  c->timing = enable == 2 ? 1 : enable != 0 ? 15 : 0;
+  if (!keep) c->evUsed[0] = c->evUsed[1] = c->evUsed[2] = c->evUsed[3] = 0;
   return VAME_OK;
 }
 
 int vame_get_timing(vame_ctx* c, int cls, double* total_ms, int* launches, int reset) {
-  if (!c || cls < 0 || cls > 2 || !total_ms || !launches) return VAME_E_INVALID;
+  if (!c || cls < 0 || cls > 3 || !total_ms || !launches) return VAME_E_INVALID;
   DeviceGuard guard(c->device);
   VAME_HIP(guard.err);
   double t = 0;

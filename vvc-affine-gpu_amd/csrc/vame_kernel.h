@@ -92,6 +92,11 @@ constexpr int kMaxPairs = 32;  // pairs per launch (kernel-argument table, 2.9 K
 struct KParams {
   PairArgs pair[kMaxPairs];
   const vame_cpmvs_dev* prev[2];  // [align]: 3-CP seeds when the 2-CP pass is not run
+  // affine_me_ctu2 (two sub-blocks per lane): the five gradient sums of every
+  // sub-block at its CU's best 2-CP iteration (3-CP seed reuse), per
+  // (pair, CTU): [nPairs * nCtus][5][1024] -- global, not LDS, so that two
+  // workgroups fit a CU
+  int32_t* bestS;
   const Item* items;
   const int32_t* order;      // [nChunks][cpp]: CTU of each padded combination slot, -1 = padding
   int nItems, nCtus, nPairs;
@@ -754,7 +759,7 @@ __device__ __forceinline__ void prof_refine(const int (&acc)[4][4], const MvFiel
 // :1096-1239, PROF off), SATD against the original (aux_functions.cl:1940-2043).
 // The prediction stays in registers (P[r] = packed sample pairs of row r) for
 // the gradient step, and so do the original samples (O[r]).
-template <int TILE, int TP, bool PROF, bool FORCE_TILE = false>
+template <int TILE, int TP, bool PROF, bool FORCE_TILE = false, int NCP = 3>
 __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, const Geo& g,
                                           const uint16_t* s_tile, int tx0, int ty0, int tmx, int tmy,
                                           const uint16_t* __restrict__ ref,
@@ -770,13 +775,24 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   }
   const int px = f.spread ? (g.w >> 1) : sx + 2, py = f.spread ? (g.h >> 1) : sy + 2;
   // |h|, |v| < 2^22 (clamped CPMVs, << (7 - log2 size)), px, py <= 128: 24-bit products are exact
-  int mx = f.bx + __mul24(f.hx, px) + __mul24(f.vx, py);
-  int my = f.by + __mul24(f.hy, px) + __mul24(f.vy, py);
+  int mx, my;
+  if constexpr (NCP == 2) {  // (vx, vy) = (-hy, hx): no negated operand
+    mx = f.bx + __mul24(f.hx, px) - __mul24(f.hy, py);
+    my = f.by + __mul24(f.hy, px) + __mul24(f.hx, py);
+  } else {
+    mx = f.bx + __mul24(f.hx, px) + __mul24(f.vx, py);
+    my = f.by + __mul24(f.hy, px) + __mul24(f.vy, py);
+  }
   mx = (mx + 64 - (mx >= 0)) >> 7;  // roundMv (aux_functions.cl:38-47)
   my = (my + 64 - (my >= 0)) >> 7;
-  clip_mv(mx, my, g.x, g.y, W, H);
-  const int ix = mx >> 4, fx = mx & 15, iy = my >> 4, fy = my & 15;
-  const int wx = g.x + sx + ix - 2, wy = g.y + sy + iy - 2;  // window origin (frame)
+  // clipMv (aux_functions.cl:51-67) on the frame position of the MV's target,
+  // 16 x the CU position + mv: its bounds [(-135 - x) << 4, (W + 7 - x) << 4]
+  // shifted by x << 4 become the frame constants [-135 << 4, (W + 7) << 4]
+  // (the shift is a multiple of 16: the fractional phase is unchanged)
+  const int ax = clampi(mx + shl(g.x, 4), -135 * 16, (W + 7) * 16);
+  const int ay = clampi(my + shl(g.y, 4), -135 * 16, (H + 7) * 16);
+  const int fx = ax & 15, fy = ay & 15;
+  const int wx = (ax >> 4) + sx - 2, wy = (ay >> 4) + sy - 2;  // window origin (frame)
   int tx = wx - tx0, ty = wy - ty0;
   if ((VAME_ABLATE & 512) || FORCE_TILE) {  // timing-only: every window read from the tile (wrong results)
     tx = clampi(tx, 0, tmx);
@@ -1148,12 +1164,16 @@ struct CuState {
 // CU: one's single-wave solve overlaps the other's prediction), its tile
 // staged over the CU's extent only (160 x 96 or 96 x 160 of the square
 // storage).
-enum { kKindQuad = 0, kKindCtu = 1, kKindHalf = 2 };
+// 3 affine_me_ctu2 -- ONE 128x128 CU per 512-thread workgroup, two
+// vertically adjacent sub-blocks per lane, two workgroups per CU (one's
+// single-wave cost and solve phases overlap the other's prediction).
+enum { kKindQuad = 0, kKindCtu = 1, kKindHalf = 2, kKindCtu2 = 3 };
 template <int KIND>
 struct Cfg {
   static constexpr int REGION = KIND == kKindQuad ? 64 : 128;  // largest region edge
-  static constexpr int THREADS = KIND == kKindQuad ? 256 : KIND == kKindCtu ? 1024 : 512;  // = sub-blocks
-  static constexpr int MAXCU = KIND == kKindHalf ? 1 : kMaxCu;  // CU state slots (LDS)
+  static constexpr int THREADS = KIND == kKindQuad ? 256 : KIND == kKindCtu ? 1024 : 512;
+  static constexpr int SBL = KIND == kKindCtu2 ? 2 : 1;  // sub-blocks per lane (stacked vertically)
+  static constexpr int MAXCU = (KIND == kKindHalf || KIND == kKindCtu2) ? 1 : kMaxCu;  // CU state slots (LDS)
   static constexpr int ITEMCU = KIND == kKindQuad ? kItemCu : MAXCU;  // CU slots per item
   static constexpr bool AUTO = KIND == kKindQuad;       // holds autonomous items
   static constexpr int MARGIN = 16;                     // reference-tile margin (samples)
@@ -1162,7 +1182,7 @@ struct Cfg {
   // apart land 16 banks apart (2-way at most for the packed-pair reads)
   static constexpr int TP = (TILE + 7) / 16 * 16 + 8;
   static constexpr int TILE_ELEMS = TILE * TP + 16;
-  static constexpr int NSB = THREADS;                   // sub-blocks per work item (max)
+  static constexpr int NSB = THREADS * SBL;             // sub-blocks per work item (max)
 };
 
 // Value i of a sub-block's contribution to its CU's normal equations
@@ -1401,8 +1421,19 @@ __device__ __forceinline__ void held_window(int lidx, int& off, int& limit) {
   }
 }
 
-template <int NCP, int LOGS, bool COOP>
-__device__ __forceinline__ void reduce_equations_64(const int (&S)[5], int u, int v, bool owner,
+// Value i of a lane's contribution: its sub-block's, or with SBL = 2 the sum
+// of its two (vertically stacked: same u, rows v[0], v[1]) -- integer sums, so
+// adding before the reduction is exact.
+template <int NCP, int SBL>
+__device__ __forceinline__ long long lane_value(int i, const int (&S)[SBL][5], int u, const int (&v)[SBL]) {
+  long long r = eq_value<NCP>(i, S[0], u, v[0]);
+#pragma unroll
+  for (int j = 1; j < SBL; j++) r += eq_value<NCP>(i, S[j], u, v[j]);
+  return r;
+}
+
+template <int NCP, int LOGS, bool COOP, int SBL>
+__device__ __forceinline__ void reduce_equations_64(const int (&S)[SBL][5], int u, const int (&v)[SBL], bool owner,
                                                     long long* dst) {
   constexpr int NV = NCP == 2 ? kNumVal2 : kNumMom;
   long long x[NV];
@@ -1416,7 +1447,7 @@ __device__ __forceinline__ void reduce_equations_64(const int (&S)[5], int u, in
     constexpr int B0 = Schedule<LOGS>::bit(0);
 #pragma unroll
     for (int j = 0; j < H; j++)
-      x[j] = pair_step<B0>(eq_value<NCP>(j, S, u, v), j + H < NV ? eq_value<NCP>(j + H, S, u, v) : 0);
+      x[j] = pair_step<B0>(lane_value<NCP, SBL>(j, S, u, v), j + H < NV ? lane_value<NCP, SBL>(j + H, S, u, v) : 0);
     butterfly64<LOGS, 1, H>(x);
   }
   constexpr int CNT = final_count<LOGS, NV>();
@@ -1449,17 +1480,17 @@ __device__ __forceinline__ void reduce_equations_64(const int (&S)[5], int u, in
   }
 }
 
-template <int NCP>
-__device__ __forceinline__ void reduce_equations(const int (&S)[5], int u, int v, int logS,
+template <int NCP, int SBL>
+__device__ __forceinline__ void reduce_equations(const int (&S)[SBL][5], int u, const int (&v)[SBL], int logS,
                                                  bool owner, bool coop, long long* dst) {
   if (coop) {  // cooperative items: whole-wave segments, partial sums meet in LDS atomics
-    reduce_equations_64<NCP, 6, true>(S, u, v, owner, dst);
+    reduce_equations_64<NCP, 6, true, SBL>(S, u, v, owner, dst);
     return;
   }
   switch (logS) {  // wave-uniform; autonomous waves hold CUs of 16, 32 or 64 sub-blocks
-    case 4: reduce_equations_64<NCP, 4, false>(S, u, v, owner, dst); break;
-    case 5: reduce_equations_64<NCP, 5, false>(S, u, v, owner, dst); break;
-    default: reduce_equations_64<NCP, 6, false>(S, u, v, owner, dst); break;
+    case 4: reduce_equations_64<NCP, 4, false, SBL>(S, u, v, owner, dst); break;
+    case 5: reduce_equations_64<NCP, 5, false, SBL>(S, u, v, owner, dst); break;
+    default: reduce_equations_64<NCP, 6, false, SBL>(S, u, v, owner, dst); break;
   }
 }
 
@@ -1474,11 +1505,19 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   (void)REGION;
   __shared__ __attribute__((aligned(16))) uint16_t s_tile[C::TILE_ELEMS];
   static_assert((C::TP * 2) % 16 == 0 && C::TILE % 8 == 0, "16-byte tile rows");
-  __shared__ uint2 s_top[C::NSB];  // row 0 of every sub-block's prediction (packed pairs)
-  __shared__ uint2 s_bot[C::NSB];  // row 3
+  // row 0 / row 3 of every lane's prediction (packed pairs): of its sub-block,
+  // or with two stacked sub-blocks per lane (SBL = 2) the upper one's top and
+  // the lower one's bottom row (their inner rows stay in the lane)
+  __shared__ uint2 s_top[C::THREADS];
+  __shared__ uint2 s_bot[C::THREADS];
   // the five gradient sums of every sub-block at its CU's best 2-CP iteration
-  // (3-CP seed reuse, see the 3-CP init)
-  __shared__ int s_bestS[5][C::NSB];
+  // (3-CP seed reuse, see the 3-CP init); SBL = 2 keeps them in p.bestS
+  constexpr int SBL = C::SBL;
+  __shared__ int s_bestS[5][SBL == 1 ? C::NSB : 1];
+  // SBL = 2: the upper sub-block's prediction, parked in LDS from its SATD to
+  // the gradient step (row r of lane t at [r][t]), so the lower one's
+  // prediction runs with no extra live registers
+  __shared__ uint2 s_pred[SBL == 2 ? 4 : 1][SBL == 2 ? C::THREADS : 1];
   __shared__ __attribute__((aligned(16))) long long s_val[C::MAXCU][kNumMom];
   __shared__ double s_mat[C::MAXCU][42];  // per CU: N x (N + 1) system, N <= 6
   __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
@@ -1644,11 +1683,13 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       g.x = ctuX + cs.x;
       g.y = ctuY + cs.y;
       // the lane's own prediction rows: a task's CUs take consecutive lanes
-      // (of the workgroup, or of the running wave), in raster order within each
+      // (of the workgroup, or of the running wave), in raster order within
+      // each (SBL = 2: a lane per column and pair of sub-block rows, its two
+      // sub-blocks at sy and sy + 4)
       sbIdx = tid;
       sbCols = 1 << (g.lw - 2);
       sx = (local & (sbCols - 1)) << 2;
-      sy = (local >> (g.lw - 2)) << 2;
+      sy = (local >> (g.lw - 2)) << (SBL == 2 ? 3 : 2);
       active = (g.x + g.w <= W) && (g.y + g.h <= H);  // affine.cl:192-193
     }
     const bool leader = myCu >= 0 && (lane & ((1 << logS) - 1)) == (1 << logS) - 1;
@@ -1742,7 +1783,9 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         // (the CU's lanes are uniformly live or not), so the whole step runs
         // under `live`: the DPP neighbour reads at the CU's edges may see lanes
         // of other CUs, whose columns the border replication discards.
-        uint2 Pr[4], Og[4];  // this lane's prediction and original rows (packed pairs)
+        // this lane's prediction and original rows (packed pairs), per sub-block
+        // (SBL = 2: the originals are read again in the gradient step)
+        uint2 Pr[SBL][4], Og[SBL][4];
         uint4 X[6];          // extended rows 0..3 (X[1..4]) and the neighbours' edges
         const bool live = active && s_st[myCu < 0 ? 0 : myCu].live;
         // 3-CP iteration 0 of a seed-reuse CU: SATD (set at init) and gradient
@@ -1756,16 +1799,26 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           int cp[6];
           for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
           const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
-          bool outside;
-          const int satdLane = predict_sb<C::TILE, C::TP, PROF, (VAME_ABLATE & 1024) != 0 && ncp == 3>(
-              f, sxp, syp, gp, s_tile, tx0, ty0, tileW - 9, tileH - 9, ref, cur, W, H, s_coef, Pr, Og, outside);
+          int satdLane = 0;
+#pragma unroll
+          for (int j = 0; j < SBL; j++) {
+            bool outside;
+            satdLane += predict_sb<C::TILE, C::TP, PROF, (VAME_ABLATE & 1024) != 0 && ncp == 3, ncp>(
+                f, sxp, syp + 4 * j, gp, s_tile, tx0, ty0, tileW - 9, tileH - 9, ref, cur, W, H, s_coef, Pr[j],
+                Og[j], outside);
+            if (SBL == 2 && j == 0) {
+#pragma unroll
+              for (int r = 0; r < 4; r++) s_pred[r][sbIdx] = Pr[0][r];
+            }
 #if VAME_COUNT_PRED
-          {  // instrumentation: windows outside the tile, per kernel and pass, one atomic per wave
-            const unsigned long long out = __builtin_amdgcn_ballot_w64(outside);
-            if (out && __lane_id() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
-              atomicAdd(&g_pred_count[2 + 2 * (REGION == 128) + (ncp == 3)], (unsigned long long)__popcll(out));
-          }
+            {  // instrumentation: windows outside the tile, per kernel and pass, one atomic per wave
+              const unsigned long long out = __builtin_amdgcn_ballot_w64(outside);
+              if (out && __lane_id() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
+                atomicAdd(&g_pred_count[2 + 2 * (REGION == 128) + (ncp == 3)], (unsigned long long)__popcll(out));
+            }
+            if (j > 0) PC_ADD
 #endif
+          }
           if (kDup & 1) {
             MvField f2 = f;
             opaque(f2.bx);
@@ -1777,12 +1830,15 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             asm volatile("" ::"v"(s2));
           }
           // extended rows (neighbour columns by DPP), edge rows published for
-          // the sub-blocks above and below
+          // the sub-blocks above and below (SBL = 2: the gradient step forms
+          // the extended rows of both sub-blocks)
+          if constexpr (SBL == 1) {
 #pragma unroll
-          for (int r = 0; r < 4; r++)
-            X[r + 1] = ext_row(Pr[r], dpp32<0x138, 0xF>((int)Pr[r].y), dpp32<0x130, 0xF>((int)Pr[r].x));
-          s_top[sbIdx] = Pr[0];
-          s_bot[sbIdx] = Pr[3];
+            for (int r = 0; r < 4; r++)
+              X[r + 1] = ext_row(Pr[0][r], dpp32<0x138, 0xF>((int)Pr[0][r].y), dpp32<0x130, 0xF>((int)Pr[0][r].x));
+          }
+          s_top[sbIdx] = Pr[0][0];
+          s_bot[sbIdx] = Pr[SBL - 1][3];
           const int v = logS == 4 ? seg_sum_c<4>(satdLane)
                         : logS == 5 ? seg_sum_c<5>(satdLane) : seg_sum_c<6>(satdLane);
           if (leader) {
@@ -1848,45 +1904,100 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
 
         // =============== gradients + normal equations (affine.cl:477-752) ===============
         {
-          int S[5] = {0, 0, 0, 0, 0};
+          int S[SBL][5];
+#pragma unroll
+          for (int j = 0; j < SBL; j++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) S[j][k] = 0;
+          // SBL = 2: the seed-reuse sums in global memory, per (pair, CTU): a
+          // uniform base and 32-bit lane offsets (recomputed, not hoisted)
+          char* gBest = SBL == 2 ? reinterpret_cast<char*>(p.bestS + (size_t)(pairIdx * p.nCtus + ctu) * 5 * C::NSB)
+                                 : nullptr;
+          auto gbest = [&](int k, int j) -> int32_t& {
+            int i = sbIdx;
+            opaque(i);
+            return *reinterpret_cast<int32_t*>(gBest + (unsigned)(k * C::NSB + j * C::THREADS + i) * 4u);
+          };
           if (reuse && live) {
 #pragma unroll
-            for (int k = 0; k < 5; k++) S[k] = s_bestS[k][sbIdx];
+            for (int j = 0; j < SBL; j++)
+#pragma unroll
+              for (int k = 0; k < 5; k++) S[j][k] = SBL == 1 ? s_bestS[k][sbIdx] : gbest(k, j);
           } else if (live && !(VAME_ABLATE & 2)) {
             // the neighbours' edge rows, extended by the left / right lanes' copies
             // the sub-blocks above / below, computed here (kept live across the
             // passes, the index was spilled)
-            const uint2 tb = s_bot[max(sbIdx - sbCols, 0)], bt = s_top[min(sbIdx + sbCols, C::NSB - 1)];
+            int nbIdx = sbIdx;
+            if constexpr (SBL == 2) opaque(nbIdx);  // recomputed, not hoisted (VGPRs)
+            const uint2 tb = s_bot[max(nbIdx - sbCols, 0)], bt = s_top[min(nbIdx + sbCols, C::THREADS - 1)];
             X[0] = ext_row(tb, dpp32<0x138, 0xF>((int)tb.y), dpp32<0x130, 0xF>((int)tb.x));
-            X[5] = ext_row(bt, dpp32<0x138, 0xF>((int)bt.y), dpp32<0x130, 0xF>((int)bt.x));
             Geo gg = g;
             int sxg = sx, syg = sy;
-            grad_sb(sxg, syg, gg, X, Og, S);
+            if constexpr (SBL == 2) opaque_geo(gg, sxg, syg);
+            if constexpr (SBL == 1) {
+              X[5] = ext_row(bt, dpp32<0x138, 0xF>((int)bt.y), dpp32<0x130, 0xF>((int)bt.x));
+              grad_sb(sxg, syg, gg, X, Og[0], S[0]);
+            } else {
+              // upper sub-block: rows X[1..4] its own, X[5] the lower one's top row;
+              // lower sub-block: X[0] the upper one's bottom row, X[5] the lane
+              // below's; the original rows read again (the frame base + 32-bit offsets)
+#pragma unroll
+              for (int j = 0; j < SBL; j++) {
+                if (j == 0) {
+#pragma unroll
+                  for (int r = 0; r < 4; r++) Pr[0][r] = s_pred[r][sbIdx];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                  X[r + 1] = ext_row(Pr[j][r], dpp32<0x138, 0xF>((int)Pr[j][r].y),
+                                     dpp32<0x130, 0xF>((int)Pr[j][r].x));
+                const uint2 nb = j + 1 < SBL ? Pr[j + 1][0] : bt;
+                X[5] = ext_row(nb, dpp32<0x138, 0xF>((int)nb.y), dpp32<0x130, 0xF>((int)nb.x));
+                {
+                  const unsigned b0 = (unsigned)((gg.y + syg + 4 * j) * W + gg.x + sxg) * 2u, bw = (unsigned)W * 2u;
+                  const char* base = reinterpret_cast<const char*>(cur);
+#pragma unroll
+                  for (int r = 0; r < 4; r++) Og[j][r] = *reinterpret_cast<const uint2*>(base + (b0 + (unsigned)r * bw));
+                }
+                grad_sb(sxg, syg + 4 * j, gg, X, Og[j], S[j]);
+                if (j + 1 < SBL) X[0] = X[4];  // the lower sub-block's row above = the upper one's row 3
+              }
+            }
             if (kDup & 2) {
               int S2[5];
               int sxd = sxg;
               opaque(sxd);
-              grad_sb(sxd, syg, gg, X, Og, S2);
+              grad_sb(sxd, syg, gg, X, Og[0], S2);
               asm volatile("" ::"v"(S2[0] ^ S2[1] ^ S2[2] ^ S2[3] ^ S2[4]));
             }
             if (keepS && better) {  // the best iteration's sums, for the 3-CP seed reuse
 #pragma unroll
-              for (int k = 0; k < 5; k++) s_bestS[k][sbIdx] = S[k];
+              for (int j = 0; j < SBL; j++)
+#pragma unroll
+                for (int k = 0; k < 5; k++) {
+                  if constexpr (SBL == 1)
+                    s_bestS[k][sbIdx] = S[j][k];
+                  else
+                    gbest(k, j) = S[j][k];
+                }
             }
           }
           if (!(VAME_ABLATE & 4)) {
             long long* dst = s_val[myCu < 0 ? 0 : myCu];
+            int va[SBL];
+#pragma unroll
+            for (int j = 0; j < SBL; j++) va[j] = sy + 2 + 4 * j;
             if (ncp == 2)
-              reduce_equations<2>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
+              reduce_equations<2, SBL>(S, sx + 2, va, logS, myCu >= 0, coop, dst);
             else
-              reduce_equations<3>(S, sx + 2, sy + 2, logS, myCu >= 0, coop, dst);
+              reduce_equations<3, SBL>(S, sx + 2, va, logS, myCu >= 0, coop, dst);
             if constexpr ((kDup & 4) != 0) {
               int ud = sx + 2;
               opaque(ud);
               if (ncp == 2)
-                reduce_equations<2>(S, ud, sy + 2, logS, myCu >= 0, coop, s_dup);
+                reduce_equations<2, SBL>(S, ud, va, logS, myCu >= 0, coop, s_dup);
               else
-                reduce_equations<3>(S, ud, sy + 2, logS, myCu >= 0, coop, s_dup);
+                reduce_equations<3, SBL>(S, ud, va, logS, myCu >= 0, coop, s_dup);
             }
           }
         }
@@ -2057,6 +2168,13 @@ __global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_bod
 template <int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_half(KParams p) {
   affine_me_body<kKindHalf, false, MODE>(p);
+}
+// ONE 128x128 CU per 512-thread workgroup, two stacked sub-blocks per lane,
+// two workgroups per CU (~72 KB of LDS each; the 3-CP seed-reuse sums in
+// global memory): 128 VGPRs so both fit.
+template <int MODE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_ctu2(KParams p) {
+  affine_me_body<kKindCtu2, false, MODE>(p);
 }
 // The same with PROF (vame_set_prof).
 template <int MODE>

@@ -18,7 +18,7 @@ EXPORTS = (
     "vame_log_writer_create", "vame_log_writer_poc", "vame_log_writer_destroy", "vame_pred_mask",
     "vame_log_writer_refs", "vame_read_frames_range", "vame_count_lines", "vame_read_frames_span",
     "vame_log_writer_set_deferred", "vame_log_writer_num_files", "vame_log_writer_file_name",
-    "vame_log_writer_sizes", "vame_log_writer_flush_at", "vame_template_coverage",
+    "vame_log_writer_sizes", "vame_log_writer_flush_at", "vame_template_coverage", "vame_pack_records",
 )
 
 
@@ -52,6 +52,7 @@ def lib():
         L.vame_affine_me.argtypes = [P, P, P, F, I, I, I, P, P, P, P]
         L.vame_affine_me_poc.argtypes = [P, P, P, I, F, I, I, ctypes.POINTER(PocResult), P]
         L.vame_affine_me_batch.argtypes = [P, ctypes.POINTER(PocJob), I, I, I, P]
+        L.vame_pack_records.argtypes = [P, ctypes.POINTER(PocJob), I, I, P, ctypes.c_longlong, P, P]
         L.vame_num_ctus.argtypes = [I, I]
         L.vame_cus_per_ctu.argtypes = [I]
         L.vame_num_groups.argtypes = [I]

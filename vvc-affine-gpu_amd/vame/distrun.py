@@ -275,7 +275,8 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
     # the compact-form check of the packed records, collected on the device and
     # read once after the last launch (a per-launch read would stall the
     # launching thread until that launch finished)
-    pack_bad = torch.zeros((), dtype=torch.bool, device=device)
+    hip_pack = hasattr(engine, "pack_records")  # the HIP engine packs in one kernel
+    pack_bad = torch.zeros((), dtype=torch.int32 if hip_pack else torch.bool, device=device)
 
     # ---- the writer thread: formats each launch's POCs once its copy landed
     slots = _HostSlots(2, cuda)
@@ -350,8 +351,11 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
                     ev.record(dnstream)
             work.put((ev, slot, batch, host))
         elif a.log:  # gather path: compact records stay on this GPU until the gather
-            slab_parts.append(shard.pack([j[3] for j in jobs], None, device, modes=modes,
-                                         validate=pack_bad))
+            if hip_pack:
+                slab_parts.append(engine.pack_records([j[3] for j in jobs], modes, None, pack_bad))
+            else:
+                slab_parts.append(shard.pack([j[3] for j in jobs], None, device, modes=modes,
+                                             validate=pack_bad))
     work.put(None)
     th.join()
     up_stop.set()

@@ -72,7 +72,8 @@ class Engine:
 
     def get_timing(self, kernel_class: int, reset: bool = True):
         """(total_ms, launches) of kernel class 0 (quadrant items, affine_me_quad) /
-        1 (128x128 CUs, affine_me_ctu) / 2 (128x64 and 64x128 CUs, affine_me_half)."""
+        1 (CTU items, affine_me_ctu) / 2 (128x64 and 64x128 CUs, affine_me_half) /
+        3 (128x128 CUs, affine_me_ctu2)."""
         t, n = ctypes.c_double(), ctypes.c_int()
         check(lib().vame_get_timing(self._h, kernel_class, ctypes.byref(t), ctypes.byref(n), int(reset)))
         return t.value, n.value
@@ -163,6 +164,38 @@ class Engine:
             arr[j].out = ctypes.cast(ctypes.pointer(pr), ctypes.c_void_p)
         check(lib().vame_affine_me_batch(self._h, arr, len(jobs), modes, extra, self._stream()))
         return [job[3] for job in jobs]
+
+    def pack_records(self, results: list[dict], modes: int, words: int | None = None,
+                     bad: torch.Tensor | None = None) -> torch.Tensor:
+        """vame_pack_records: the POCs' results (alloc_poc dicts, POC order) in
+        the compact wire form of shard.pack, one kernel, zero-padded to
+        `words`; `bad` (int32 device scalar) is OR-ed with 1 when a record does
+        not fit the form (shard.check_flag reads it)."""
+        from .shard import slab_words
+        need = slab_words([(max(r for r, _ in res) + 1, modes, (self.n_cus(0), self.n_cus(1)))
+                           for res in results])
+        words = need if words is None else words
+        if words < need:
+            raise ValueError("slab larger than the agreed size")
+        slab = torch.empty(words, dtype=torch.int32, device=self.device)
+        if bad is None:
+            bad = torch.zeros((), dtype=torch.int32, device=self.device)
+        arr = (PocJob * max(len(results), 1))()
+        keep = []
+        for j, res in enumerate(results):
+            nrefs = max(r for r, _ in res) + 1
+            self._check_poc_out(res, nrefs, modes)
+            pr = PocResult()
+            for (r, name), (cost, cpmv) in res.items():
+                m = MODES.index(name)
+                pr.cost[r][m] = cost.data_ptr()
+                pr.cpmvs[r][m] = cpmv.data_ptr()
+            keep.append(pr)
+            arr[j].nrefs = nrefs
+            arr[j].out = ctypes.cast(ctypes.pointer(pr), ctypes.c_void_p)
+        check(lib().vame_pack_records(self._h, arr, len(results), modes, slab.data_ptr(), words,
+                                      bad.data_ptr(), self._stream()))
+        return slab
 
     def affine_me_poc(self, cur, refs, lam: float, modes: int = 3, extra: int = 0, out=None):
         """modes: 1 = 2-CP only, 3 = 2-CP then 3-CP, plus MODE_FULL / MODE_HALF to

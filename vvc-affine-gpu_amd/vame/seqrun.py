@@ -92,7 +92,14 @@ class ShardRun:
             self.eng.affine_me_batch(self.jobs, self.modes, 0)
 
     def slab(self) -> torch.Tensor:
-        """This rank's decision records packed into its compact slab (on the GPU)."""
+        """This rank's decision records packed into its compact slab: on the
+        GPU in one kernel (vame_pack_records), or by shard.pack (its
+        specification) for an engine without one."""
+        if hasattr(self.eng, "pack_records"):
+            bad = torch.zeros((), dtype=torch.int32, device=self.device)
+            slab = self.eng.pack_records([j[3] for j in self.jobs], self.modes, self.words, bad)
+            shard.check_flag(bad)
+            return slab
         return shard.pack([j[3] for j in self.jobs], self.words, self.device, modes=self.modes)
 
     def exchange(self, slab: torch.Tensor):
