@@ -1183,6 +1183,12 @@ struct Cfg {
   static constexpr int TP = (TILE + 7) / 16 * 16 + 8;
   static constexpr int TILE_ELEMS = TILE * TP + 16;
   static constexpr int NSB = THREADS * SBL;             // sub-blocks per work item (max)
+#ifndef VAME_STASH
+#define VAME_STASH 1
+#endif
+  // SBL = 2: the upper sub-block's prediction parked in LDS across the lower
+  // one's (VAME_STASH=0: held in registers)
+  static constexpr bool STASH = VAME_STASH != 0;
 };
 
 // Value i of a sub-block's contribution to its CU's normal equations
@@ -1517,7 +1523,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   // SBL = 2: the upper sub-block's prediction, parked in LDS from its SATD to
   // the gradient step (row r of lane t at [r][t]), so the lower one's
   // prediction runs with no extra live registers
-  __shared__ uint2 s_pred[SBL == 2 ? 4 : 1][SBL == 2 ? C::THREADS : 1];
+  constexpr bool STASH = SBL == 2 && C::STASH;
+  __shared__ uint2 s_pred[STASH ? 4 : 1][STASH ? C::THREADS : 1];
   __shared__ __attribute__((aligned(16))) long long s_val[C::MAXCU][kNumMom];
   __shared__ double s_mat[C::MAXCU][42];  // per CU: N x (N + 1) system, N <= 6
   __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
@@ -1808,7 +1815,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
                 Og[j], outside);
             if (SBL == 2 && j == 0) {
 #pragma unroll
-              for (int r = 0; r < 4; r++) s_pred[r][sbIdx] = Pr[0][r];
+              for (int r = 0; r < 4; r++)
+                if constexpr (STASH) s_pred[r][sbIdx] = Pr[0][r];
             }
 #if VAME_COUNT_PRED
             {  // instrumentation: windows outside the tile, per kernel and pass, one atomic per wave
@@ -1943,7 +1951,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
               // below's; the original rows read again (the frame base + 32-bit offsets)
 #pragma unroll
               for (int j = 0; j < SBL; j++) {
-                if (j == 0) {
+                if (STASH && j == 0) {
 #pragma unroll
                   for (int r = 0; r < 4; r++) Pr[0][r] = s_pred[r][sbIdx];
                 }
