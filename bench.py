@@ -216,17 +216,19 @@ def main():
         step_ms = [elapsed * 1e3 / max(args.steps, 1)]
     quad_ms, quad_n = eng.get_timing(0)
     # the 128-class kernels (CTU items: affine_me_ctu, class 1; 128x64 /
-    # 64x128 CUs: affine_me_half, class 2; 128x128 CUs: affine_me_ctu2, class
-    # 3), timed in the sampled timed steps with VAME_BENCH_KTIMING=1, else on
-    # extra untimed steps after them
-    big_t = {k: eng.get_timing(k) for k in (1, 2, 3)}
+    # 64x128 CUs: affine_me_half, class 2, or affine_me_half2w / _half2h,
+    # classes 4 / 5; 128x128 CUs: affine_me_ctu2, class 3), timed in the
+    # sampled timed steps with VAME_BENCH_KTIMING=1, else on extra untimed
+    # steps after them
+    BIG = (1, 2, 3, 4, 5)
+    big_t = {k: eng.get_timing(k) for k in BIG}
     big_on = "the sampled timed steps"
     if ktiming != 1:
         big_steps = min(args.steps, 20)
         eng.set_timing(True)
         for _ in range(big_steps):
             run.step()
-        big_t = {k: eng.get_timing(k) for k in (1, 2, 3)}
+        big_t = {k: eng.get_timing(k) for k in BIG}
         eng.get_timing(0)
         big_on = f"{big_steps} untimed steps after the timed ones"
     eng.set_timing(False)
@@ -292,12 +294,14 @@ def main():
     # launches).  A step mixing both packings leaves the CTU kernel's bytes
     # unattributed.
     ctu2 = big_t[3][1] > 0
-    split = big_t[2][1] > 0
-    mixed = split and (big_t[2][1] != big_t[1][1] if not ctu2 else big_t[1][1] > 0)
+    split = big_t[2][1] > 0 or big_t[4][1] > 0
+    n_half = big_t[2][1] or big_t[4][1]
+    mixed = split and (n_half != big_t[1][1] if not ctu2 else big_t[1][1] > 0)
     ctu_key = ("bytes_half" if ctu2 else "bytes_ctu") if split or ctu2 else "bytes_big"
     big_kernels = {}
     for k, name, key in ((1, "affine_me_ctu", ctu_key), (2, "affine_me_half", "bytes_half"),
-                         (3, "affine_me_ctu2", "bytes_ctu")):
+                         (3, "affine_me_ctu2", "bytes_ctu"), (4, "affine_me_half2w", "bytes_half_w"),
+                         (5, "affine_me_half2h", "bytes_half_h")):
         ms, n = big_t[k]
         if n == 0 or (mixed and k == 1):
             continue

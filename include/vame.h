@@ -67,7 +67,7 @@ typedef struct {
  * defaults are the measured best on MI355X): work packing
  * VAME_TASKS (wave tasks per autonomous quadrant item, 1..16, default 16),
  * VAME_CLAIM, VAME_CHAIN, VAME_MIX (default 1 each), VAME_HALF128, VAME_CTU2,
- * VAME_HALF_MIN_PAIRS; launch structure VAME_STREAMS, VAME_QUAD_FIRST,
+ * VAME_HALF2, VAME_HALF_MIN_PAIRS; launch structure VAME_STREAMS, VAME_QUAD_FIRST,
  * VAME_GRAPH, VAME_JOIN_EACH; block order VAME_ITEM_ORDER, VAME_XCD_ORDER, VAME_GROUP_COMBOS,
  * VAME_GROUP_COMBOS_BIG. */
 int vame_create(vame_ctx** out, int device, int width, int height);
@@ -130,9 +130,10 @@ int vame_set_prof(vame_ctx* ctx, int enable);
  * own dispatch on the stream it runs on.  kernel_class 0 = quadrant work items
  * (affine_me_quad); 1 = CTU items (affine_me_ctu: every 128-class CU in launches
  * of fewer than VAME_HALF_MIN_PAIRS pairs); 2 = single 128x64 / 64x128 CUs
- * (affine_me_half) and 3 = single 128x128 CUs (affine_me_ctu2), both in
- * launches of at least VAME_HALF_MIN_PAIRS pairs (VAME_HALF128 / VAME_CTU2
- * select the other packings).
+ * (affine_me_half, with VAME_HALF2=0), 3 = single 128x128 CUs
+ * (affine_me_ctu2), 4 / 5 = single 128x64 / 64x128 CUs (affine_me_half2w /
+ * _half2h): 2 / 4 / 5 and 3 in launches of at least VAME_HALF_MIN_PAIRS pairs
+ * (VAME_HALF128 / VAME_CTU2 / VAME_HALF2 select the other packings).
  * enable = 2 times the quadrant kernel only (its dispatches carry the events;
  * the 128-class launches run untimed).  vame_get_timing waits for the recorded
  * launches and returns their summed duration and count since the last reset.

@@ -88,7 +88,8 @@ def timed_dispatches(d):
     lps = ts.get("launches_per_step")  # the quadrant kernel's launches per step (sampled events)
     launches = {"affine_me_quad": roof.get("launches")}
     events = {"affine_me_quad": roof.get("avg_launch_ms")}
-    for k in ("affine_me_ctu", "affine_me_half", "affine_me_ctu2"):  # the 128-class kernels (their own steps)
+    for k in ("affine_me_ctu", "affine_me_half", "affine_me_ctu2", "affine_me_half2w",
+              "affine_me_half2h"):  # the 128-class kernels (timed on their own steps)
         launches[k] = roof.get(k, {}).get("launches")
         events[k] = roof.get(k, {}).get("avg_launch_ms")
     out = {}

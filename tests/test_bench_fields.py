@@ -32,12 +32,14 @@ def test_roofline_fractions_from_profile(path):
     p = json.load(open(path))
     pc = p.get("pred_count") or {}
     timed = lambda k: bool((p["kernels"].get(k) or {}).get("timed_avg_ms"))  # noqa: E731
-    half, ctu2 = timed("affine_me_half"), timed("affine_me_ctu2")
+    half, ctu2 = timed("affine_me_half") or timed("affine_me_half2w"), timed("affine_me_ctu2")
     keys = {"affine_me_quad": ("bytes_quad", pc.get("executed_pred_frac_quad")),
             "affine_me_ctu": (("bytes_half" if ctu2 else "bytes_ctu") if half or ctu2 else "bytes_big",
                               pc.get("executed_pred_frac_ctu")),
             "affine_me_half": ("bytes_half", pc.get("executed_pred_frac_ctu")),
-            "affine_me_ctu2": ("bytes_ctu", pc.get("executed_pred_frac_ctu"))}
+            "affine_me_ctu2": ("bytes_ctu", pc.get("executed_pred_frac_ctu")),
+            "affine_me_half2w": ("bytes_half_w", pc.get("executed_pred_frac_ctu")),
+            "affine_me_half2h": ("bytes_half_h", pc.get("executed_pred_frac_ctu"))}
     seen = 0
     for name, (key, ex) in keys.items():
         k = p["kernels"].get(name) or {}

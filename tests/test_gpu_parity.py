@@ -440,12 +440,12 @@ def test_property_translation_1080p(engines, d):
                                  {"VAME_TASKS": "8"}, {"VAME_TASKS": "4", "VAME_CHAIN": "0", "VAME_MIX": "0"},
                                  {"VAME_TASKS": "1"}, {"VAME_CLAIM": "0"}, {"VAME_ITEM_ORDER": "0"},
                                  {"VAME_CTU2": "2"}, {"VAME_CTU2": "0", "VAME_HALF128": "1"},
-                                 {"VAME_GRAPH": "1", "VAME_CTU2": "2"}],
+                                 {"VAME_GRAPH": "1", "VAME_CTU2": "2"}, {"VAME_HALF128": "1", "VAME_HALF2": "0"}],
                          ids=["half512_packing", "ctu1024_packing", "two_streams", "two_streams_half512",
                               "ctu_first", "graph", "graph_half512", "graph_two_streams", "aligns_unmixed",
                               "items_of_8", "items_of_4_unchained_unmixed", "items_of_1_task",
                               "static_tasks", "items_by_quadrant", "ctu2_in_short_launches",
-                              "ctu1024_128x128_half512", "graph_ctu2_in_short_launches"])
+                              "ctu1024_128x128_half512", "graph_ctu2_in_short_launches", "half512_one_sb_per_lane"])
 def test_launch_structure_variants(env, monkeypatch):
     """The engine's launch-structure knobs (read at vame_create) change only
     where the work runs: VAME_HALF128=1 gives every 128x64 / 64x128 CU a
@@ -457,7 +457,9 @@ def test_launch_structure_variants(env, monkeypatch):
     VAME_QUAD_FIRST=0 issues the 128-class kernels before the quadrant kernel;
     VAME_CTU2=2 runs the 128x128 CUs in affine_me_ctu2 (512 threads, two
     stacked sub-blocks per lane; by default only in launches of >= 16 pairs)
-    and 0 never;
+    and 0 never; VAME_HALF2=0 runs the half packing's 128x64 / 64x128 CUs in
+    affine_me_half (512 threads, one sub-block per lane) instead of
+    affine_me_half2w / _half2h (256 threads, two per lane);
     VAME_TASKS=8 / 4 / 1 packs 8 / 4 / 1 wave tasks per autonomous quadrant
     item (default 16 over the one staged tile, each wave claiming the next
     task as it finishes; VAME_CLAIM=0: wave w runs tasks w, w + 4, ...),

@@ -44,7 +44,14 @@ struct vame_ctx {
   Item* dBig1 = nullptr;
   Item* dBig2 = nullptr;  // dBig3 without the 128x128 item (that one runs in affine_me_ctu2)
   Item* dHalf = nullptr;
-  int nQuadFull = 0, nQuadHalf = 0, nQuadBoth = 0, nBig3 = 0, nBig1 = 0, nBig2 = 0, nHalf = 0;
+  Item* dHalfW = nullptr;  // dHalf's 128x64 / 64x128 items (affine_me_half2w / _half2h)
+  Item* dHalfH = nullptr;
+  int nQuadFull = 0, nQuadHalf = 0, nQuadBoth = 0, nBig3 = 0, nBig1 = 0, nBig2 = 0, nHalf = 0, nHalfW = 0,
+      nHalfH = 0;
+  // VAME_HALF2 (default 1): the 128x64 / 64x128 CUs of the half packing in
+  // affine_me_half2w / _half2h (256 threads, two stacked sub-blocks per lane,
+  // four workgroups per CU) instead of affine_me_half (512 threads, one per lane)
+  bool half2 = true;
   // VAME_CTU2: where the 128x128 CUs run -- 1 (default): in affine_me_ctu2
   // (512 threads, two stacked sub-blocks per lane, two workgroups per CU) in
   // the launches that use affine_me_half (>= halfMinPairs pairs), in the CTU
@@ -73,8 +80,9 @@ struct vame_ctx {
   hipStream_t side = nullptr;   // second stream: 128-class items run beside the quadrant items
   hipEvent_t evFork = nullptr, evJoin = nullptr;
   // optional per-kernel timing: (start, end) event pairs per kernel class
-  // (0 quadrant, 1 CTU items, 2 128x64 / 64x128 CUs, 3 128x128 CUs in
-  // affine_me_ctu2)
+  // (0 quadrant, 1 CTU items, 2 128x64 / 64x128 CUs in affine_me_half, 3
+  // 128x128 CUs in affine_me_ctu2, 4 / 5 128x64 / 64x128 CUs in
+  // affine_me_half2w / _half2h)
   int timing = 0;
   // PROF on (vame_set_prof): the *_prof kernels
   bool prof = false;
@@ -98,8 +106,8 @@ struct vame_ctx {
     hipGraphExec_t exec;
   };
   std::vector<GraphEntry> graphs;  // most recent last, at most kMaxGraphs
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[4];
-  size_t evUsed[4] = {0, 0, 0, 0};
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[6];
+  size_t evUsed[6] = {0, 0, 0, 0, 0, 0};
   // vame_pack_records: the segment table of the last pack (host copy kept
   // until the next call) and its device copy
   std::vector<struct PackSeg> packSegs;
@@ -486,7 +494,13 @@ std::vector<int32_t> build_order(int nCtus, int cols, int groupCombos, int xcdOr
 using KernelFn = void (*)(KParams);
 template <int KIND>
 KernelFn kernel_for(bool prof, int mode) {
-  if constexpr (KIND == kKindCtu2) {
+  if constexpr (KIND == kKindHalf2W) {
+    (void)prof;
+    return mode == 1 ? affine_me_half2w<1> : mode == 2 ? affine_me_half2w<2> : affine_me_half2w<3>;
+  } else if constexpr (KIND == kKindHalf2H) {
+    (void)prof;
+    return mode == 1 ? affine_me_half2h<1> : mode == 2 ? affine_me_half2h<2> : affine_me_half2h<3>;
+  } else if constexpr (KIND == kKindCtu2) {
     (void)prof;  // PROF runs the 128x128 CUs in affine_me_ctu_prof (launch_direct)
     return mode == 1 ? affine_me_ctu2<1> : mode == 2 ? affine_me_ctu2<2> : affine_me_ctu2<3>;
   } else if constexpr (KIND == kKindCtu) {
@@ -508,6 +522,7 @@ constexpr size_t kMaxGraphs = 8;
 template <typename K>
 hipError_t launch_kernel(K kernel, unsigned grid, unsigned threads, hipStream_t s, hipEvent_t t0, hipEvent_t t1,
                          int flags, const KParams& kp, bool capture) {
+  if (grid == 0) return hipSuccess;  // no work items (a kernel class without CUs)
   if (capture)
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, kp);
   else
@@ -548,6 +563,7 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
   auto big = [&](const KParams& kp) -> int {
     KParams kb = kp;
     const bool ctu2 = !c->prof && (c->ctu2 == 2 || (c->ctu2 == 1 && use_half(kp)));
+    if (ctu2 && kp.run2 && kp.run3 && !c->bestS) return VAME_E_INVALID;  // seed-reuse scratch missing
     if (ctu2) {  // the 128x128 CUs in affine_me_ctu2, the rest (short launches) in CTU items
       kb.items = c->dBig1;
       kb.nItems = c->nBig1;
@@ -573,6 +589,23 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
     return VAME_OK;
   };
   auto half = [&](const KParams& kp) -> int {  // after the 128x128 items, on their stream
+    if (c->half2 && !c->prof) {  // 128x64 then 64x128 CUs, 256-thread workgroups
+      if (kp.run2 && kp.run3 && !c->bestS) return VAME_E_INVALID;  // seed-reuse scratch missing
+      for (int o = 0; o < 2; o++) {
+        KParams kh = kp;
+        kh.items = o ? c->dHalfH : c->dHalfW;
+        kh.nItems = o ? c->nHalfH : c->nHalfW;
+        kh.bestS = c->bestS ? c->bestS + (size_t)kMaxPairs * c->nCtus * 5 * (Cfg<kKindCtu2>::NSB +
+                                                                              o * 2 * Cfg<kKindHalf2W>::NSB)
+                            : nullptr;
+        const unsigned grid = block_grid(c, 1, kh);
+        hipEvent_t t0, t1;
+        VAME_TRY(time_events(c, 4 + o, t0, t1));
+        VAME_HIP(launch_kernel(o ? kernel_for<kKindHalf2H>(false, mode) : kernel_for<kKindHalf2W>(false, mode),
+                               grid, Cfg<kKindHalf2W>::THREADS, sBig, t0, t1, order_flag(), kh, capture));
+      }
+      return VAME_OK;
+    }
     KParams kh = kp;
     kh.items = c->dHalf;
     kh.nItems = c->nHalf;
@@ -630,9 +663,12 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
 
 int launch(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool quadHalf, bool bigItems,
            hipStream_t stream) {
-  if (c->ctu2 && !c->bestS && bigItems && !kps.empty() && kps[0].run2 && kps[0].run3) {
-    // affine_me_ctu2's 3-CP seed-reuse sums: 5 x 1024 int32 per (pair, CTU) of a launch
-    VAME_HIP(hipMalloc(&c->bestS, (size_t)kMaxPairs * c->nCtus * 5 * Cfg<kKindCtu2>::NSB * sizeof(int32_t)));
+  if ((c->ctu2 || c->half2) && !c->bestS && bigItems && !kps.empty() && kps[0].run2 && kps[0].run3) {
+    // the 3-CP seed-reuse sums of the kernels with two sub-blocks per lane,
+    // 5 int32 per sub-block: per (pair, CTU) of a launch the 128x128 CU
+    // (affine_me_ctu2), then the two 128x64 and the two 64x128 CUs (_half2w / _half2h)
+    VAME_HIP(hipMalloc(&c->bestS, (size_t)kMaxPairs * c->nCtus * 5 *
+                                      (Cfg<kKindCtu2>::NSB + 4 * Cfg<kKindHalf2W>::NSB) * sizeof(int32_t)));
   }
   if (!c->useGraph || c->timing || kps.empty()) return launch_direct(c, kps, quadFull, quadHalf, bigItems, stream, false);
   // the call's identity: its kernel arguments and launch selection
@@ -732,6 +768,9 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   qh.clear();
   qb.clear();
   build_templates(big1, hf, qf, qh, qb, true, tasks, chain_coop(), mix_aligns());
+  std::vector<Item> hfw, hfh;  // the single-CU half items by orientation
+  for (const Item& it : hf) (it.cu[0].lw > it.cu[0].lh ? hfw : hfh).push_back(it);
+  if (hfw.empty() || hfh.empty()) return VAME_E_INVALID;
   vame_ctx* c = new vame_ctx();
   c->device = device;
   c->W = width;
@@ -743,6 +782,9 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   c->nBig2 = (int)big2.size();
   c->ctu2 = std::min(2, std::max(0, env_int("VAME_CTU2", 1)));
   c->nHalf = (int)hf.size();
+  c->nHalfW = (int)hfw.size();
+  c->nHalfH = (int)hfh.size();
+  c->half2 = env_int("VAME_HALF2", 1) != 0;
   c->halfMode = std::min(2, std::max(0, env_int("VAME_HALF128", 2)));
   c->halfMinPairs = std::max(1, env_int("VAME_HALF_MIN_PAIRS", 16));
   c->nQuadFull = (int)qf.size();
@@ -774,6 +816,12 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (e == hipSuccess) e = hipMemcpy(c->dQuad, quad.data(), quad.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->dBig3, big3.data(), big3.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->dBig1, big1.data(), big1.size() * sizeof(Item), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !hfw.empty()) e = hipMalloc(&c->dHalfW, hfw.size() * sizeof(Item));
+  if (e == hipSuccess && !hfw.empty())
+    e = hipMemcpy(c->dHalfW, hfw.data(), hfw.size() * sizeof(Item), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !hfh.empty()) e = hipMalloc(&c->dHalfH, hfh.size() * sizeof(Item));
+  if (e == hipSuccess && !hfh.empty())
+    e = hipMemcpy(c->dHalfH, hfh.data(), hfh.size() * sizeof(Item), hipMemcpyHostToDevice);
   if (e == hipSuccess && !hf.empty()) e = hipMalloc(&c->dHalf, hf.size() * sizeof(Item));
   if (e == hipSuccess && !hf.empty())
     e = hipMemcpy(c->dHalf, hf.data(), hf.size() * sizeof(Item), hipMemcpyHostToDevice);
@@ -799,6 +847,8 @@ void vame_destroy(vame_ctx* c) {
   if (c->dBig2) (void)hipFree(c->dBig2);
   if (c->bestS) (void)hipFree(c->bestS);
   if (c->dHalf) (void)hipFree(c->dHalf);
+  if (c->dHalfW) (void)hipFree(c->dHalfW);
+  if (c->dHalfH) (void)hipFree(c->dHalfH);
   for (int k = 0; k < 2; k++)
     if (c->dOrder[k]) (void)hipFree(c->dOrder[k]);
   for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
@@ -808,7 +858,7 @@ void vame_destroy(vame_ctx* c) {
   if (c->evJoin) (void)hipEventDestroy(c->evJoin);
   if (c->dPackSegs) (void)hipFree(c->dPackSegs);
   if (c->packEv) (void)hipEventDestroy(c->packEv);
-  for (int k = 0; k < 4; k++)
+  for (int k = 0; k < 6; k++)
     for (auto& e : c->ev[k]) {
       (void)hipEventDestroy(e.first);
       (void)hipEventDestroy(e.second);
@@ -999,13 +1049,14 @@ int vame_set_timing(vame_ctx* c, int enable) {
   // a sample of its steps toggles timing between them)
   const bool keep = (enable & VAME_TIMING_KEEP) != 0;
   enable &= ~VAME_TIMING_KEEP;
-  c->timing = enable == 2 ? 1 : enable != 0 ? 15 : 0;
-  if (!keep) c->evUsed[0] = c->evUsed[1] = c->evUsed[2] = c->evUsed[3] = 0;
+  c->timing = enable == 2 ? 1 : enable != 0 ? 63 : 0;
+  if (!keep)
+    for (size_t& u : c->evUsed) u = 0;
   return VAME_OK;
 }
 
 int vame_get_timing(vame_ctx* c, int cls, double* total_ms, int* launches, int reset) {
-  if (!c || cls < 0 || cls > 3 || !total_ms || !launches) return VAME_E_INVALID;
+  if (!c || cls < 0 || cls > 5 || !total_ms || !launches) return VAME_E_INVALID;
   DeviceGuard guard(c->device);
   VAME_HIP(guard.err);
   double t = 0;

@@ -92,10 +92,10 @@ constexpr int kMaxPairs = 32;  // pairs per launch (kernel-argument table, 2.9 K
 struct KParams {
   PairArgs pair[kMaxPairs];
   const vame_cpmvs_dev* prev[2];  // [align]: 3-CP seeds when the 2-CP pass is not run
-  // affine_me_ctu2 (two sub-blocks per lane): the five gradient sums of every
-  // sub-block at its CU's best 2-CP iteration (3-CP seed reuse), per
-  // (pair, CTU): [nPairs * nCtus][5][1024] -- global, not LDS, so that two
-  // workgroups fit a CU
+  // kernels with two sub-blocks per lane (affine_me_ctu2 / _half2w / _half2h):
+  // the five gradient sums of every sub-block at its CU's best 2-CP iteration
+  // (3-CP seed reuse), per (pair, CTU, item): [nPairs * nCtus * nItems][5][NSB]
+  // -- global, not LDS, so that two / four workgroups fit a CU
   int32_t* bestS;
   const Item* items;
   const int32_t* order;      // [nChunks][cpp]: CTU of each padded combination slot, -1 = padding
@@ -1167,28 +1167,35 @@ struct CuState {
 // 3 affine_me_ctu2 -- ONE 128x128 CU per 512-thread workgroup, two
 // vertically adjacent sub-blocks per lane, two workgroups per CU (one's
 // single-wave cost and solve phases overlap the other's prediction).
-enum { kKindQuad = 0, kKindCtu = 1, kKindHalf = 2, kKindCtu2 = 3 };
+// 4 / 5 affine_me_half2w / affine_me_half2h -- ONE 128x64 / 64x128 CU per
+// 256-thread workgroup, two stacked sub-blocks per lane, its tile staged over
+// the CU's extent (160 x 96 / 96 x 160, sized for it), four workgroups per CU.
+enum { kKindQuad = 0, kKindCtu = 1, kKindHalf = 2, kKindCtu2 = 3, kKindHalf2W = 4, kKindHalf2H = 5 };
 template <int KIND>
 struct Cfg {
+  static constexpr bool HALF2 = KIND == kKindHalf2W || KIND == kKindHalf2H;
   static constexpr int REGION = KIND == kKindQuad ? 64 : 128;  // largest region edge
-  static constexpr int THREADS = KIND == kKindQuad ? 256 : KIND == kKindCtu ? 1024 : 512;
-  static constexpr int SBL = KIND == kKindCtu2 ? 2 : 1;  // sub-blocks per lane (stacked vertically)
-  static constexpr int MAXCU = (KIND == kKindHalf || KIND == kKindCtu2) ? 1 : kMaxCu;  // CU state slots (LDS)
+  static constexpr int THREADS = KIND == kKindQuad || HALF2 ? 256 : KIND == kKindCtu ? 1024 : 512;
+  static constexpr int SBL = KIND == kKindCtu2 || HALF2 ? 2 : 1;  // sub-blocks per lane (stacked vertically)
+  static constexpr int MAXCU = (KIND == kKindHalf || KIND == kKindCtu2 || HALF2) ? 1 : kMaxCu;  // CU state slots (LDS)
   static constexpr int ITEMCU = KIND == kKindQuad ? kItemCu : MAXCU;  // CU slots per item
   static constexpr bool AUTO = KIND == kKindQuad;       // holds autonomous items
   static constexpr int MARGIN = 16;                     // reference-tile margin (samples)
-  static constexpr int TILE = REGION + 2 * MARGIN;      // tile edge (samples)
+  static constexpr int TILE = REGION + 2 * MARGIN;      // tile edge (samples; the staged extent's largest)
+  static constexpr int TILE_W = KIND == kKindHalf2H ? 64 + 2 * MARGIN : TILE;  // allocated tile extent
+  static constexpr int TILE_H = KIND == kKindHalf2W ? 64 + 2 * MARGIN : TILE;
   // tile pitch (samples) == 8 (mod 16): the window rows of sub-blocks 4 rows
   // apart land 16 banks apart (2-way at most for the packed-pair reads)
-  static constexpr int TP = (TILE + 7) / 16 * 16 + 8;
-  static constexpr int TILE_ELEMS = TILE * TP + 16;
+  static constexpr int TP = (TILE_W + 7) / 16 * 16 + 8;
+  static constexpr int TILE_ELEMS = TILE_H * TP + 16;
   static constexpr int NSB = THREADS * SBL;             // sub-blocks per work item (max)
 #ifndef VAME_STASH
 #define VAME_STASH 1
 #endif
   // SBL = 2: the upper sub-block's prediction parked in LDS across the lower
   // one's (VAME_STASH=0: held in registers)
-  static constexpr bool STASH = VAME_STASH != 0;
+  // (affine_me_half2*: in registers, so that four workgroups fit a CU's LDS)
+  static constexpr bool STASH = VAME_STASH != 0 && !HALF2;
 };
 
 // Value i of a sub-block's contribution to its CU's normal equations
@@ -1510,7 +1517,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   constexpr int REGION = C::REGION;  // instrumentation slots: 128 = the 128-class kernels
   (void)REGION;
   __shared__ __attribute__((aligned(16))) uint16_t s_tile[C::TILE_ELEMS];
-  static_assert((C::TP * 2) % 16 == 0 && C::TILE % 8 == 0, "16-byte tile rows");
+  static_assert((C::TP * 2) % 16 == 0 && C::TILE_W % 8 == 0, "16-byte tile rows");
   // row 0 / row 3 of every lane's prediction (packed pairs): of its sub-block,
   // or with two stacked sub-blocks per lane (SBL = 2) the upper one's top and
   // the lower one's bottom row (their inner rows stay in the lane)
@@ -1577,11 +1584,11 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   const bool regionOut = tx0 + C::MARGIN >= W || ty0 + C::MARGIN >= H;
   // the staged extent: the whole square tile, or (affine_me_half) the CU's
   // region + margin, a 160 x 96 or 96 x 160 part of the square storage
-  const int tileW = KIND == kKindHalf ? (int)it->rw + 2 * C::MARGIN : C::TILE;
-  const int tileH = KIND == kKindHalf ? (int)it->rh + 2 * C::MARGIN : C::TILE;
+  const int tileW = KIND == kKindHalf ? (int)it->rw + 2 * C::MARGIN : C::TILE_W;
+  const int tileH = KIND == kKindHalf ? (int)it->rh + 2 * C::MARGIN : C::TILE_H;
   const int CPR = tileW / 8;  // chunks per tile row
   const int NCH = tileH * CPR;
-  constexpr int PER = (C::TILE * (C::TILE / 8) + C::THREADS - 1) / C::THREADS;
+  constexpr int PER = (C::TILE_H * (C::TILE_W / 8) + C::THREADS - 1) / C::THREADS;
   uint4 tv[PER];
   if constexpr ((VAME_DUP & 64) != 0) {  // timing-only: one extra staging round trip
     if (!regionOut) {
@@ -1919,7 +1926,8 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             for (int k = 0; k < 5; k++) S[j][k] = 0;
           // SBL = 2: the seed-reuse sums in global memory, per (pair, CTU): a
           // uniform base and 32-bit lane offsets (recomputed, not hoisted)
-          char* gBest = SBL == 2 ? reinterpret_cast<char*>(p.bestS + (size_t)(pairIdx * p.nCtus + ctu) * 5 * C::NSB)
+          char* gBest = SBL == 2 ? reinterpret_cast<char*>(p.bestS + ((size_t)(pairIdx * p.nCtus + ctu) * p.nItems +
+                                                                      itemIdx) * 5 * C::NSB)
                                  : nullptr;
           auto gbest = [&](int k, int j) -> int32_t& {
             int i = sbIdx;
@@ -2183,6 +2191,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
 template <int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_ctu2(KParams p) {
   affine_me_body<kKindCtu2, false, MODE>(p);
+}
+// ONE 128x64 (w) / 64x128 (h) CU per 256-thread workgroup, two stacked
+// sub-blocks per lane, four workgroups per CU (~40 KB of LDS each).
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_half2w(KParams p) {
+  affine_me_body<kKindHalf2W, false, MODE>(p);
+}
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_half2h(KParams p) {
+  affine_me_body<kKindHalf2H, false, MODE>(p);
 }
 // The same with PROF (vame_set_prof).
 template <int MODE>

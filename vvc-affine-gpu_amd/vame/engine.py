@@ -73,7 +73,8 @@ class Engine:
     def get_timing(self, kernel_class: int, reset: bool = True):
         """(total_ms, launches) of kernel class 0 (quadrant items, affine_me_quad) /
         1 (CTU items, affine_me_ctu) / 2 (128x64 and 64x128 CUs, affine_me_half) /
-        3 (128x128 CUs, affine_me_ctu2)."""
+        3 (128x128 CUs, affine_me_ctu2) / 4, 5 (128x64 / 64x128 CUs,
+        affine_me_half2w / affine_me_half2h)."""
         t, n = ctypes.c_double(), ctypes.c_int()
         check(lib().vame_get_timing(self._h, kernel_class, ctypes.byref(t), ctypes.byref(n), int(reset)))
         return t.value, n.value

@@ -38,7 +38,8 @@ def pair_accounting(W: int, H: int, ncps=(2,), extra: int = 0):
     128x128 CUs of affine_me_ctu, 'half' = the 128x64 / 64x128 CUs of
     affine_me_half)."""
     acc = {"rows": 0, "rows_inframe": 0, "bytes_quad": 0, "bytes_big": 0, "bytes_ctu": 0,
-           "bytes_half": 0, "sb_pred": 0, "sb_pred_quad": 0, "sb_pred_big": 0}
+           "bytes_half": 0, "bytes_half_w": 0, "bytes_half_h": 0, "sb_pred": 0, "sb_pred_quad": 0,
+           "sb_pred_big": 0}
     inv = cu_inventory(W, H)
     for ncp in ncps:
         npred = N_PRED[ncp] + extra
@@ -54,5 +55,7 @@ def pair_accounting(W: int, H: int, ncps=(2,), extra: int = 0):
             acc["bytes_big" if big else "bytes_quad"] += b
             if big:
                 acc["bytes_ctu" if w == h else "bytes_half"] += b
+                if w != h:  # 128x64 (affine_me_half2w) / 64x128 (affine_me_half2h)
+                    acc["bytes_half_w" if w > h else "bytes_half_h"] += b
     acc["bytes"] = acc["bytes_quad"] + acc["bytes_big"]
     return acc
