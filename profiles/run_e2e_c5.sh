@@ -6,8 +6,8 @@
 #   2. `vame.distrun --gpus 8 --rank-only K` for K = 0 and 7: one rank's share
 #      of the 8-GPU frame shard alone on this GPU and its 16-CPU share --
 #      ingest of its frames, its kernel time and the formatting of its own
-#      log block (--shard-logs): what each rank of an 8-GPU node does;
-#   3. the 40 files of a 2-rank distrun (gloo, one GPU, --shard-logs) compared
+#      log block (the default log path): what each rank of an 8-GPU node does;
+#   3. the 40 files of a 2-rank distrun (gloo, one GPU) compared
 #      byte for byte with the CLI's.
 #   bash profiles/run_e2e_c5.sh <tag> [frames]
 set -euo pipefail
@@ -44,9 +44,9 @@ done
 if [ "$F" -le 60 ]; then
   mkdir -p $T/d2
   VAME_DIST_BACKEND=gloo timeout -k 10 600 python3 -m vame.distrun -f $F -s 3840x2160 -q 32 -o $T/orig.csv \
-      -r $T/recon.csv -l $T/d2/log --gpus 2 --shard-logs > $O/distrun2_shard.txt
+      -r $T/recon.csv -l $T/d2/log --gpus 2 > $O/distrun2_shard.txt
   grep -E "EXEC|OVERALL|READ_CSV|LOG_WRITE|LOG_MERGE|LOG_BYTES" $O/distrun2_shard.txt
   for f in $(ls $T/cli); do cmp -s $T/cli/$f $T/d2/$f || { echo "MISMATCH $f"; exit 1; }; done
-  echo "distrun --gpus 2 --shard-logs: $(ls $T/d2 | wc -l) files byte-identical to the CLI's"
+  echo "distrun --gpus 2: $(ls $T/d2 | wc -l) files byte-identical to the CLI's"
 fi
 echo e2e-c5-done

@@ -539,37 +539,56 @@ int vame_log_writer_sizes(vame_log_writer* w, long long* sizes) {
 long long vame_log_writer_flush_at(vame_log_writer* w, const long long* offsets) {
   if (!w || !offsets) return VAME_E_INVALID;
   std::atomic<int> bad{0};
-  std::atomic<long long> total{0};
+  long long total = 0;
   w->held.resize(w->paths.size());
-  w->pool->run((int)w->paths.size(), [&](int f) {
+  // one task per held block (not per file: the 40 files' sizes differ by two
+  // orders of magnitude, the 16x16 groups' files hold most of the bytes), each
+  // written at its own offset -- the files opened once, never truncated
+  struct Piece {
+    int f;
+    const char* q;
+    size_t n;
+    long long off;
+  };
+  std::vector<Piece> pieces;
+  std::vector<int> fds(w->paths.size(), -1);
+  for (size_t f = 0; f < w->paths.size(); f++) {
     vame_log_writer::Held& h = w->held[f];
-    if (!h.total) return;
-    const int fd = open(w->paths[f].c_str(), O_WRONLY | O_CREAT, 0644);  // never truncated
-    if (fd < 0) {
+    if (!h.total) continue;
+    fds[f] = open(w->paths[f].c_str(), O_WRONLY | O_CREAT, 0644);
+    if (fds[f] < 0) {
       bad = 1;
-      return;
+      break;
     }
     long long off = offsets[f];
     for (size_t b = 0; b < h.blocks.size(); b++) {
-      const char* q = h.blocks[b].get();
-      size_t left = b + 1 == h.blocks.size() ? h.last : vame_log_writer::kHeldBlock;
+      const size_t n = b + 1 == h.blocks.size() ? h.last : vame_log_writer::kHeldBlock;
+      pieces.push_back({(int)f, h.blocks[b].get(), n, off});
+      off += (long long)n;
+    }
+    total += h.total;
+  }
+  if (!bad)
+    w->pool->run((int)pieces.size(), [&](int i) {
+      const Piece& pc = pieces[i];
+      const char* q = pc.q;
+      size_t left = pc.n;
+      long long off = pc.off;
       while (left) {
-        const ssize_t k = pwrite(fd, q, left, (off_t)off);
+        const ssize_t k = pwrite(fds[pc.f], q, left, (off_t)off);
         if (k <= 0) {
           bad = 1;
-          close(fd);
           return;
         }
         q += k;
         off += k;
         left -= (size_t)k;
       }
-    }
-    close(fd);
-    total += h.total;
-    h = vame_log_writer::Held();
-  });
-  return bad ? VAME_E_INVALID : total.load();
+    });
+  for (int fd : fds)
+    if (fd >= 0) close(fd);
+  for (auto& h : w->held) h = vame_log_writer::Held();
+  return bad ? VAME_E_INVALID : total;
 }
 
 int vame_log_writer_destroy(vame_log_writer* w) {
