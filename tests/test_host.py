@@ -143,3 +143,54 @@ def test_build_record_matches_the_library():
     want = rec["artefacts"]["vvc-affine-gpu_amd/lib/libvame.so"]["sha256"]
     assert hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest() == want
     assert rec["mode"].startswith("rebuilt")
+
+
+def kernel_scratch(lib_path):
+    """{kernel: private_segment_fixed_size} from the gfx950 code object inside
+    a built library (the clang offload bundle in its fat binary, the AMDGPU
+    metadata note read by llvm-readelf)."""
+    import struct
+    import subprocess
+    import tempfile
+    d = open(lib_path, "rb").read()
+    i = d.find(b"__CLANG_OFFLOAD_BUNDLE__")
+    assert i >= 0, "no offload bundle in " + lib_path
+    n = struct.unpack_from("<Q", d, i + 24)[0]
+    p = i + 32
+    for _ in range(n):
+        off, size, idl = struct.unpack_from("<QQQ", d, p)
+        p += 24
+        ident = d[p:p + idl].decode()
+        p += idl
+        if "gfx950" not in ident:
+            continue
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(d[i + off:i + off + size])
+            f.flush()
+            out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", f.name],
+                                 capture_output=True, text=True, check=True).stdout
+        names = re.findall(r"\.name:\s+(\S+)", out)
+        priv = [int(v) for v in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", out)]
+        assert len(names) == len(priv) and names
+        return dict(zip(names, priv))
+    raise AssertionError("no gfx950 code object in " + lib_path)
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-readelf"), reason="no llvm-readelf")
+def test_product_kernels_have_no_scratch():
+    """zero scratch in the product kernels rests on the build's
+    -disable-machine-licm and on the kernels' opaque() recomputation, so a
+    compiler update or a kernel edit that brings spills back fails here: every
+    affine_me_* kernel of the built libvame.so has a zero private segment,
+    except affine_me_half2w / _half2h, whose upper sub-block's prediction stays
+    in registers across the lower one's (16-20 B per lane; parked
+    in LDS instead they ran 8 % slower, three workgroups per CU instead of
+    four), and the PROF variants (not the benchmarked path)."""
+    sizes = kernel_scratch(_lib.LIB_PATH)
+    product = {k: v for k, v in sizes.items() if "affine_me" in k and "prof" not in k}
+    assert len(product) == 18, sorted(product)
+    for k, v in product.items():
+        if "half2" in k:
+            assert v <= 24, (k, v)
+        else:
+            assert v == 0, (k, v)

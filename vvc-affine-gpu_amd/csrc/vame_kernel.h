@@ -1194,8 +1194,12 @@ struct Cfg {
 #endif
   // SBL = 2: the upper sub-block's prediction parked in LDS across the lower
   // one's (VAME_STASH=0: held in registers)
-  // (affine_me_half2*: in registers, so that four workgroups fit a CU's LDS)
-  static constexpr bool STASH = VAME_STASH != 0 && !HALF2;
+  // (affine_me_half2*: in registers, so that four workgroups fit a CU's LDS;
+  // VAME_HALF2_STASH=1 parks it there too, three workgroups per CU)
+#ifndef VAME_HALF2_STASH
+#define VAME_HALF2_STASH 0
+#endif
+  static constexpr bool STASH = VAME_STASH != 0 && (!HALF2 || VAME_HALF2_STASH != 0);
 };
 
 // Value i of a sub-block's contribution to its CU's normal equations
