@@ -43,3 +43,16 @@ if bound:
     bound.sort()
     print(f"step-boundary idle: median {bound[len(bound) // 2] / 1e3:.1f} us, min {bound[0] / 1e3:.1f}, "
           f"max {bound[-1] / 1e3:.1f} us over {len(bound)} boundaries")
+# per step, each kernel's start / end relative to the step's first start (median over the steps)
+names = sorted({n for _, _, n in iv})
+rel = {n: [] for n in names}
+for st in steps:
+    t0 = min(s for s, _, _ in st)
+    for s, e, n in st:
+        rel[n].append(((s - t0) / 1e3, (e - t0) / 1e3))
+print("timeline (us from the step's first start, median):")
+for n in names:
+    if rel[n]:
+        ss = sorted(x for x, _ in rel[n])
+        ee = sorted(y for _, y in rel[n])
+        print(f"  {n.split('(')[0][:48]:48s} start {ss[len(ss) // 2]:8.1f}  end {ee[len(ee) // 2]:8.1f}")

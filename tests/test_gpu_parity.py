@@ -239,18 +239,20 @@ def test_live_reference_configs(engines, tmp_path, W, H, qp, poc, refidx, extra)
     job = (dev(orig[poc]), d_refs, lam, eng.alloc_poc(len(refs), 3))
     eng.affine_me_batch([job], 3, extra)
     check_vs_live_reference(runs, job[3], lambda name: (refidx, name), recon[rp], orig[poc], lam, extra)
-    # both packings of the 128-class CUs: this short launch ran the CTU items;
-    # the long launches of the configs run affine_me_half (VAME_HALF128=1 here)
+    # both packings of the 128-class CUs: the default (affine_me_ctu2 and
+    # affine_me_half2w / _half2h) ran above; the 1024-thread CTU items here
     from vame.engine import Engine
-    old = os.environ.get("VAME_HALF128")
-    os.environ["VAME_HALF128"] = "1"
+    knobs = {"VAME_HALF128": "0", "VAME_CTU2": "0"}
+    old = {k: os.environ.get(k) for k in knobs}
+    os.environ.update(knobs)
     try:
         eng_half = Engine(W, H, 0)
     finally:
-        if old is None:
-            del os.environ["VAME_HALF128"]
-        else:
-            os.environ["VAME_HALF128"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     try:
         job_h = (job[0], d_refs, lam, eng_half.alloc_poc(len(refs), 3))
         eng_half.affine_me_batch([job_h], 3, extra)
@@ -433,33 +435,39 @@ def test_property_translation_1080p(engines, d):
     assert n > 1000 and frac >= 0.75, (frac, n)
 
 
-@pytest.mark.parametrize("env", [{"VAME_HALF128": "1"}, {"VAME_HALF128": "0"}, {"VAME_STREAMS": "2"},
-                                 {"VAME_STREAMS": "2", "VAME_HALF128": "1"}, {"VAME_QUAD_FIRST": "0"},
-                                 {"VAME_GRAPH": "1"}, {"VAME_GRAPH": "1", "VAME_HALF128": "1"},
-                                 {"VAME_GRAPH": "1", "VAME_STREAMS": "2"}, {"VAME_MIX": "0"},
-                                 {"VAME_TASKS": "8"}, {"VAME_TASKS": "4", "VAME_CHAIN": "0", "VAME_MIX": "0"},
-                                 {"VAME_TASKS": "1"}, {"VAME_CLAIM": "0"}, {"VAME_ITEM_ORDER": "0"},
-                                 {"VAME_CTU2": "2"}, {"VAME_CTU2": "0", "VAME_HALF128": "1"},
-                                 {"VAME_GRAPH": "1", "VAME_CTU2": "2"}, {"VAME_HALF128": "1", "VAME_HALF2": "0"}],
-                         ids=["half512_packing", "ctu1024_packing", "two_streams", "two_streams_half512",
-                              "ctu_first", "graph", "graph_half512", "graph_two_streams", "aligns_unmixed",
+@pytest.mark.parametrize("env", [{"VAME_HALF128": "0", "VAME_CTU2": "0"}, {"VAME_HALF128": "0"},
+                                 {"VAME_HALF128": "2", "VAME_CTU2": "1"}, {"VAME_CTU2": "0"},
+                                 {"VAME_HALF2": "0"}, {"VAME_STREAMS": "1"},
+                                 {"VAME_STREAMS": "1", "VAME_QUAD_FIRST": "0"}, {"VAME_STREAMS": "3"},
+                                 {"VAME_STREAMS": "4"}, {"VAME_STREAMS": "5"}, {"VAME_SYNC": "0"}, {"VAME_SYNC": "2"},
+                                 {"VAME_STREAMS": "4", "VAME_SYNC": "2", "VAME_JOIN_EACH": "1"},
+                                 {"VAME_GRAPH": "1"}, {"VAME_GRAPH": "1", "VAME_STREAMS": "4"},
+                                 {"VAME_GRAPH": "1", "VAME_STREAMS": "1", "VAME_HALF128": "0", "VAME_CTU2": "0"},
+                                 {"VAME_MIX": "0"}, {"VAME_TASKS": "8"},
+                                 {"VAME_TASKS": "4", "VAME_CHAIN": "0", "VAME_MIX": "0"}, {"VAME_TASKS": "1"},
+                                 {"VAME_CLAIM": "0"}, {"VAME_ITEM_ORDER": "0"}],
+                         ids=["ctu1024_items", "ctu2_and_ctu1024_items", "packing_by_launch_size", "ctu1024_128x128",
+                              "half512_one_sb_per_lane", "one_stream", "one_stream_128_class_first",
+                              "three_streams", "four_streams", "128_class_on_side_stream", "event_joins",
+                              "value_fork_and_joins", "four_streams_value_sync_join_each", "graph",
+                              "graph_four_streams", "graph_one_stream_ctu1024_items", "aligns_unmixed",
                               "items_of_8", "items_of_4_unchained_unmixed", "items_of_1_task",
-                              "static_tasks", "items_by_quadrant", "ctu2_in_short_launches",
-                              "ctu1024_128x128_half512", "graph_ctu2_in_short_launches", "half512_one_sb_per_lane"])
+                              "static_tasks", "items_by_quadrant"])
 def test_launch_structure_variants(env, monkeypatch):
     """The engine's launch-structure knobs (read at vame_create) change only
-    where the work runs: VAME_HALF128=1 gives every 128x64 / 64x128 CU a
-    512-thread affine_me_half workgroup of its own, 0 keeps them in the
-    1024-thread CTU items (two CUs per workgroup; the default for launches of
-    fewer than 16 pairs, as here); VAME_STREAMS=2 forks a side stream for the
-    quadrant kernel instead of issuing every kernel of a call on the caller's
-    stream (all but the first without the AQL barrier bit, the default);
-    VAME_QUAD_FIRST=0 issues the 128-class kernels before the quadrant kernel;
-    VAME_CTU2=2 runs the 128x128 CUs in affine_me_ctu2 (512 threads, two
-    stacked sub-blocks per lane; by default only in launches of >= 16 pairs)
-    and 0 never; VAME_HALF2=0 runs the half packing's 128x64 / 64x128 CUs in
-    affine_me_half (512 threads, one sub-block per lane) instead of
-    affine_me_half2w / _half2h (256 threads, two per lane);
+    where the work runs (defaults: the 128x128 CUs in affine_me_ctu2, every
+    128x64 / 64x128 CU in an affine_me_half2w / _half2h workgroup of its own,
+    the quadrant kernel on a side stream, the joins as stream memory
+    operations): VAME_HALF128=0 keeps the 128x64 / 64x128 CUs in 1024-thread
+    CTU items (2: by launch size), VAME_CTU2=0 runs the 128x128 CUs in them
+    too (1: by launch size); VAME_HALF2=0 runs the half packing in
+    affine_me_half (512 threads, one sub-block per lane); VAME_STREAMS=1
+    issues every kernel on the caller's stream (all but the first without the
+    AQL barrier bit; VAME_QUAD_FIRST=0: the 128-class kernels first), 3 / 4
+    give the 128x64 / 64x128 kernels side streams of their own, 5 puts the
+    128-class kernels on the side stream and the quadrant kernel on the
+    caller's; VAME_SYNC=0 joins with events, 2 forks by a stream memory
+    operation too (VAME_JOIN_EACH=1: fork and join around every launch);
     VAME_TASKS=8 / 4 / 1 packs 8 / 4 / 1 wave tasks per autonomous quadrant
     item (default 16 over the one staged tile, each wave claiming the next
     task as it finishes; VAME_CLAIM=0: wave w runs tasks w, w + 4, ...),

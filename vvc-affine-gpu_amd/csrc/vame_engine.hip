@@ -52,23 +52,21 @@ struct vame_ctx {
   // affine_me_half2w / _half2h (256 threads, two stacked sub-blocks per lane,
   // four workgroups per CU) instead of affine_me_half (512 threads, one per lane)
   bool half2 = true;
-  // VAME_CTU2: where the 128x128 CUs run -- 1 (default): in affine_me_ctu2
-  // (512 threads, two stacked sub-blocks per lane, two workgroups per CU) in
-  // the launches that use affine_me_half (>= halfMinPairs pairs), in the CTU
-  // items in shorter ones (the 3-pair c2 step: there the 128-class work is
-  // under two rounds of workgroups and a kernel more only adds a tail); 2:
-  // always in affine_me_ctu2; 0: always in CTU items.  affine_me_ctu2's 3-CP
-  // seed-reuse sums live in bestS (kMaxPairs x nCtus x 5 x 1024 int32,
-  // allocated on first use)
-  int ctu2 = 1;
+  // VAME_CTU2: where the 128x128 CUs run -- 2 (default): in affine_me_ctu2
+  // (512 threads, two stacked sub-blocks per lane, two workgroups per CU,
+  // room beside them for quadrant workgroups); 1: there in the launches that
+  // use the half packing, in the CTU items in the others; 0: always in CTU
+  // items.  The 3-CP seed-reuse sums of the two-sub-block kernels live in
+  // bestS (allocated on first use)
+  int ctu2 = 2;
   int32_t* bestS = nullptr;
-  // which packing a launch uses (VAME_HALF128): 0 always dBig3, 1 always
-  // dBig1 + dHalf, 2 (default) dBig1 + dHalf for launches of at least
-  // halfMinPairs (POC, refIdx) pairs (VAME_HALF_MIN_PAIRS, default 16), dBig3
-  // below: a short launch (the 3-pair c2 step) ends sooner with the 128-class
-  // work in the early-starting CTU items, a long one (32 pairs) gains from the
-  // smaller workgroups sharing CUs
-  int halfMode = 2, halfMinPairs = 16;
+  // which packing a launch uses (VAME_HALF128): 1 (default) always dBig1 +
+  // dHalf (every 128x64 / 64x128 CU a workgroup of its own), 0 always dBig3
+  // (1024-thread CTU items, a whole CU each), 2 dBig1 + dHalf for launches of
+  // at least halfMinPairs (POC, refIdx) pairs (VAME_HALF_MIN_PAIRS, default
+  // 16), dBig3 below.  With the quadrant kernel on its own stream the small
+  // workgroups share CUs with it (c2 0.931 vs 0.987 ms)
+  int halfMode = 1, halfMinPairs = 16;
   // VAME_QUAD_FIRST (one-stream mode, default 1): the quadrant kernel issued
   // first (it carries the call's barrier bit, the 128-class kernels follow it
   // in any order)
@@ -77,8 +75,27 @@ struct vame_ctx {
   // slot -> CTU table, group size, CTU chunks, slots per (pair, chunk)
   int32_t* dOrder[2] = {nullptr, nullptr};
   int groupCombos[2] = {408, 408}, nChunks[2] = {1, 1}, cpp[2] = {0, 0};
-  hipStream_t side = nullptr;   // second stream: 128-class items run beside the quadrant items
-  hipEvent_t evFork = nullptr, evJoin = nullptr;
+  // side streams of a call (VAME_STREAMS > 1): [0] the quadrant kernel, [1]
+  // / [2] the 128x64 / 64x128 kernels; forked from the caller's stream and
+  // joined back into it
+  hipStream_t side[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t evFork = nullptr, evJoin[3] = {nullptr, nullptr, nullptr};
+  // VAME_SYNC (default 1): the joins as stream memory operations -- the side
+  // stream writes a sequence number to a signal-memory word
+  // (hipStreamWriteValue32, ordered after its earlier work), the caller's
+  // stream waits for it (hipStreamWaitValue32) -- ~6 us per cross-stream hop
+  // on MI355X against ~12 with an event record + hipStreamWaitEvent
+  // (profiles/ubench/stream_hop.hip).  The fork stays an event: its slower
+  // hop is the head start that lets the 128-class workgroups, issued on the
+  // caller's stream, take their CUs before the quadrant kernel fills the GPU
+  // (with the fork as a value too, VAME_SYNC=2, the c2 step takes 0.99 ms
+  // instead of 0.935: the 128x128 kernel then waits for CUs until the
+  // quadrant kernel ends).  0, words that cannot be allocated, or stream
+  // capture (VAME_GRAPH): events.  syncWord[0] the fork, [1 + i] side stream
+  // i's join.
+  int valueSync = 1;
+  uint32_t* syncWord[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint32_t forkSeq = 0, joinSeq[3] = {0, 0, 0};
   // optional per-kernel timing: (start, end) event pairs per kernel class
   // (0 quadrant, 1 CTU items, 2 128x64 / 64x128 CUs in affine_me_half, 3
   // 128x128 CUs in affine_me_ctu2, 4 / 5 128x64 / 64x128 CUs in
@@ -88,13 +105,18 @@ struct vame_ctx {
   bool prof = false;
   // VAME_JOIN_EACH=1: join the two streams after every launch of a batch
   bool joinEach = false;
-  // Streams of a call (VAME_STREAMS): 1 (default) -- every kernel on the
-  // caller's stream, all but the call's first without the AQL barrier bit
-  // (hipExtAnyOrderLaunch), so they overlap with no fork / join between
-  // streams (a c2 step boundary idles ~6 us instead of ~18); 2 -- the
-  // 128-class kernels on the caller's stream, the quadrant kernel on a side
-  // stream forked from it and joined at the end of the call
-  int streams = 1;
+  // Streams of a call (VAME_STREAMS).  Kernels of one stream run one after
+  // the other on MI355X even without the AQL barrier bit
+  // (hipExtAnyOrderLaunch: profiles/ubench/anyorder_overlap.hip, three 50-us
+  // kernels take 155 us on one stream, ~90 on three), so the kernel classes
+  // of a call go to streams of their own: 4 (default) -- the quadrant kernel
+  // on side stream 0, the 128x128 CUs (affine_me_ctu2 / CTU items) on the
+  // caller's stream, the 128x64 and 64x128 kernels on side streams 1 and 2;
+  // 3 -- both of those on side stream 1; 2 -- every 128-class kernel on the
+  // caller's stream; 1 -- every kernel on the caller's stream, all but the
+  // call's first without the barrier bit.  The side streams fork from the
+  // caller's stream and join back into it at the end of the call.
+  int streams = 4;
   // VAME_GRAPH=1: a call's launch sequence (fork, kernels, join) is captured
   // once into a hipGraph (on capStream) and replayed on the caller's stream
   // whenever the same call -- the same kernel arguments -- repeats, e.g. the
@@ -532,34 +554,75 @@ hipError_t launch_kernel(K kernel, unsigned grid, unsigned threads, hipStream_t 
 
 int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, bool quadHalf, bool bigItems,
                   hipStream_t stream, bool capture) {
-  // 128-class items (big LDS, 1 workgroup per CU) and quadrant items run on
-  // two streams so they overlap: the 128-class kernel on the caller's stream,
-  // first, and the quadrant kernel on the side stream.  A 128-class
-  // workgroup needs a whole CU (16 waves, 81 KB LDS): issued first, its
-  // workgroups take CUs before the quadrant ones fill them, and the small
-  // quadrant workgroups, not the long 128-class ones, make the tail
-  // (batched c2 step 1.32 -> 1.245 ms).  The launches of one batch (32 pairs
-  // each) fork once and join once: launch k + 1's kernels follow launch k's on
-  // their own streams, so the 128-class workgroups left at the end of a
-  // launch share the GPU with the next launch's quadrant kernel instead of
-  // draining it alone.
+  // The 128-class kernels run on the caller's stream and the quadrant kernel
+  // on a side stream forked from it (VAME_STREAMS, see vame_ctx): the
+  // 128-class workgroups, issued first and ahead of the fork's cross-stream
+  // hop, take their CUs before the quadrant workgroups fill the GPU, and the
+  // quadrant workgroups then fill the room beside them (a 512-thread
+  // affine_me_ctu2 workgroup leaves a CU room for two quadrant workgroups, a
+  // 256-thread half2 one for three).  Kernels of one stream run one after the
+  // other, so only separate streams overlap them.  The launches of one batch
+  // (32 pairs each) fork once and join once: launch k + 1's kernels follow
+  // launch k's on their own streams.
   if (VAME_ABLATE & 16) bigItems = false;  // timing-only builds
   if (VAME_ABLATE & 32) quadFull = quadHalf = false;
   if (kps.empty()) return VAME_OK;
   const int mode = (kps[0].run2 ? 1 : 0) | (kps[0].run3 ? 2 : 0);  // the kernel instance (MODE)
   if (mode == 0) return VAME_OK;
-  const bool fork = c->streams != 1 && bigItems && (quadFull || quadHalf);
-  int issued = 0;  // VAME_STREAMS=1: kernels after a call's first may start before it ends
-  auto order_flag = [&]() { return c->streams == 1 && issued++ > 0 ? hipExtAnyOrderLaunch : 0; };
-  hipStream_t sBig = stream, sQuad = stream;
-  if (fork) {
-    VAME_HIP(hipEventRecord(c->evFork, stream));
-    VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
-    sQuad = c->side;
-  }
   auto use_half = [&](const KParams& kp) {
     return c->halfMode == 1 || (c->halfMode == 2 && kp.nPairs >= c->halfMinPairs);
   };
+  bool anyHalf = false;
+  for (const KParams& kp : kps) anyHalf |= bigItems && use_half(kp);
+  // the side streams this call uses: 0 the quadrant kernel, 1 / 2 the
+  // 128x64 / 64x128 kernels (VAME_STREAMS, see vame_ctx)
+  bool used[3] = {false, false, false};
+  hipStream_t sBig = stream, sQuad = stream, sHalf[2] = {stream, stream};
+  if (c->streams == 5 && bigItems && (quadFull || quadHalf)) {  // the 128-class kernels on the side stream
+    sBig = sHalf[0] = sHalf[1] = c->side[0];
+    used[0] = true;
+  } else if (c->streams > 1 && bigItems && (quadFull || quadHalf)) {
+    sQuad = c->side[0];
+    used[0] = true;
+  }
+  if (c->streams > 2 && c->streams < 5 && anyHalf) {
+    sHalf[0] = c->side[1];
+    sHalf[1] = c->side[c->streams > 3 ? 2 : 1];
+    used[1] = true;
+    used[2] = c->streams > 3;
+  }
+  const bool fork = used[0] || used[1] || used[2];
+  int issued = 0;  // VAME_STREAMS=1: kernels after a call's first may start before it ends
+  auto order_flag = [&]() { return c->streams == 1 && issued++ > 0 ? hipExtAnyOrderLaunch : 0; };
+  const bool valueSync = c->valueSync != 0 && !capture;
+  auto fork_sides = [&]() -> int {
+    if (c->valueSync == 2 && valueSync) {
+      const uint32_t v = ++c->forkSeq;
+      VAME_HIP(hipStreamWriteValue32(stream, c->syncWord[0], v, 0));
+      for (int i = 0; i < 3; i++)
+        if (used[i]) VAME_HIP(hipStreamWaitValue32(c->side[i], c->syncWord[0], v, hipStreamWaitValueGte, 0xFFFFFFFFu));
+      return VAME_OK;
+    }
+    VAME_HIP(hipEventRecord(c->evFork, stream));
+    for (int i = 0; i < 3; i++)
+      if (used[i]) VAME_HIP(hipStreamWaitEvent(c->side[i], c->evFork, 0));
+    return VAME_OK;
+  };
+  auto join_sides = [&]() -> int {
+    for (int i = 0; i < 3; i++)
+      if (used[i]) {
+        if (valueSync) {
+          const uint32_t v = ++c->joinSeq[i];
+          VAME_HIP(hipStreamWriteValue32(c->side[i], c->syncWord[1 + i], v, 0));
+          VAME_HIP(hipStreamWaitValue32(stream, c->syncWord[1 + i], v, hipStreamWaitValueGte, 0xFFFFFFFFu));
+        } else {
+          VAME_HIP(hipEventRecord(c->evJoin[i], c->side[i]));
+          VAME_HIP(hipStreamWaitEvent(stream, c->evJoin[i], 0));
+        }
+      }
+    return VAME_OK;
+  };
+  if (fork) VAME_TRY(fork_sides());
   auto big = [&](const KParams& kp) -> int {
     KParams kb = kp;
     const bool ctu2 = !c->prof && (c->ctu2 == 2 || (c->ctu2 == 1 && use_half(kp)));
@@ -602,7 +665,7 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
         hipEvent_t t0, t1;
         VAME_TRY(time_events(c, 4 + o, t0, t1));
         VAME_HIP(launch_kernel(o ? kernel_for<kKindHalf2H>(false, mode) : kernel_for<kKindHalf2W>(false, mode),
-                               grid, Cfg<kKindHalf2W>::THREADS, sBig, t0, t1, order_flag(), kh, capture));
+                               grid, Cfg<kKindHalf2W>::THREADS, sHalf[o], t0, t1, order_flag(), kh, capture));
       }
       return VAME_OK;
     }
@@ -612,7 +675,7 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
     const unsigned grid = block_grid(c, 1, kh);
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 2, t0, t1));
-    VAME_HIP(launch_kernel(kernel_for<kKindHalf>(c->prof, mode), grid, Cfg<kKindHalf>::THREADS, sBig, t0, t1,
+    VAME_HIP(launch_kernel(kernel_for<kKindHalf>(c->prof, mode), grid, Cfg<kKindHalf>::THREADS, sHalf[0], t0, t1,
                            order_flag(), kh, capture));
     return VAME_OK;
   };
@@ -640,23 +703,19 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
       if (bigItems && use_half(kps[k])) VAME_TRY(half(kps[k]));
       if (!quadFirst && (quadFull || quadHalf)) VAME_TRY(quad(kps[k]));
       if (fork && (c->joinEach || k + 1 == kps.size())) {
-        VAME_HIP(hipEventRecord(c->evJoin, c->side));
-        VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
-        if (k + 1 < kps.size()) {  // VAME_JOIN_EACH: fork again for the next launch
-          VAME_HIP(hipEventRecord(c->evFork, stream));
-          VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
-        }
+        VAME_TRY(join_sides());
+        if (k + 1 < kps.size()) VAME_TRY(fork_sides());  // VAME_JOIN_EACH: fork again for the next launch
       }
     }
     return VAME_OK;
   };
   const int rc = all();
   if (rc != VAME_OK && fork) {
-    // a launch failed after earlier quadrant kernels went to the side stream:
-    // order them before the caller's stream anyway, so the caller never frees
-    // or reuses result buffers they still write (best effort, the first error
-    // is the one reported)
-    if (hipEventRecord(c->evJoin, c->side) == hipSuccess) (void)hipStreamWaitEvent(stream, c->evJoin, 0);
+    // a launch failed after earlier kernels went to the side streams: order
+    // them before the caller's stream anyway, so the caller never frees or
+    // reuses result buffers they still write (best effort, the first error is
+    // the one reported)
+    (void)join_sides();
   }
   return rc;
 }
@@ -780,12 +839,12 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   c->nBig3 = (int)big3.size();
   c->nBig1 = (int)big1.size();
   c->nBig2 = (int)big2.size();
-  c->ctu2 = std::min(2, std::max(0, env_int("VAME_CTU2", 1)));
+  c->ctu2 = std::min(2, std::max(0, env_int("VAME_CTU2", 2)));
   c->nHalf = (int)hf.size();
   c->nHalfW = (int)hfw.size();
   c->nHalfH = (int)hfh.size();
   c->half2 = env_int("VAME_HALF2", 1) != 0;
-  c->halfMode = std::min(2, std::max(0, env_int("VAME_HALF128", 2)));
+  c->halfMode = std::min(2, std::max(0, env_int("VAME_HALF128", 1)));
   c->halfMinPairs = std::max(1, env_int("VAME_HALF_MIN_PAIRS", 16));
   c->nQuadFull = (int)qf.size();
   c->nQuadHalf = (int)qh.size();
@@ -797,7 +856,7 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   // tuning knobs of the block order (defaults measured on MI355X)
   const int xcdOrder = env_int("VAME_XCD_ORDER", 0);
   c->joinEach = env_int("VAME_JOIN_EACH", 0) != 0;
-  c->streams = env_int("VAME_STREAMS", 1) == 2 ? 2 : 1;
+  c->streams = std::min(5, std::max(1, env_int("VAME_STREAMS", 2)));
   c->useGraph = env_int("VAME_GRAPH", 0) != 0;
   c->quadFirst = env_int("VAME_QUAD_FIRST", 1) != 0;
   c->groupCombos[0] = std::max(8, env_int("VAME_GROUP_COMBOS", 408));
@@ -825,9 +884,19 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (e == hipSuccess && !hf.empty()) e = hipMalloc(&c->dHalf, hf.size() * sizeof(Item));
   if (e == hipSuccess && !hf.empty())
     e = hipMemcpy(c->dHalf, hf.data(), hf.size() * sizeof(Item), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  for (int i = 0; i < 3 && e == hipSuccess; i++) {
+    e = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin[i], hipEventDisableTiming);
+  }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming);
+  c->valueSync = std::min(2, std::max(0, env_int("VAME_SYNC", 1)));
+  for (int i = 0; i < 4 && e == hipSuccess && c->valueSync; i++) {
+    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->syncWord[i]), 8, hipMallocSignalMemory) != hipSuccess ||
+        hipMemset(c->syncWord[i], 0, 8) != hipSuccess) {
+      (void)hipGetLastError();
+      c->valueSync = 0;  // events instead
+    }
+  }
   if (e == hipSuccess && c->useGraph) e = hipStreamCreateWithFlags(&c->capStream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     snprintf(g_hip_err, sizeof(g_hip_err), "%s", hipGetErrorString(e));
@@ -853,9 +922,13 @@ void vame_destroy(vame_ctx* c) {
     if (c->dOrder[k]) (void)hipFree(c->dOrder[k]);
   for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
   if (c->capStream) (void)hipStreamDestroy(c->capStream);
-  if (c->side) (void)hipStreamDestroy(c->side);
+  for (int i = 0; i < 3; i++) {
+    if (c->side[i]) (void)hipStreamDestroy(c->side[i]);
+    if (c->evJoin[i]) (void)hipEventDestroy(c->evJoin[i]);
+  }
   if (c->evFork) (void)hipEventDestroy(c->evFork);
-  if (c->evJoin) (void)hipEventDestroy(c->evJoin);
+  for (uint32_t* w : c->syncWord)
+    if (w) (void)hipFree(w);
   if (c->dPackSegs) (void)hipFree(c->dPackSegs);
   if (c->packEv) (void)hipEventDestroy(c->packEv);
   for (int k = 0; k < 6; k++)
@@ -1086,13 +1159,14 @@ const char* vame_strerror(int code) {
 const char* vame_last_hip_error(void) { return g_hip_err; }
 
 #if VAME_PHASE_TIMING
-// profiling-only builds: per-phase shader-clock sums [kernel quad / ctu / half][pass phase] (see vame_kernel.h)
-int vame_debug_phase_cycles(unsigned long long* out48, int reset) {
-  if (!out48) return VAME_E_INVALID;
+// profiling-only builds: per-phase shader-clock sums [kernel: quad, ctu, half,
+// ctu2, half2w, half2h][pass phase ...] (see vame_kernel.h)
+int vame_debug_phase_cycles(unsigned long long* out96, int reset) {
+  if (!out96) return VAME_E_INVALID;
   VAME_HIP(hipDeviceSynchronize());
-  VAME_HIP(hipMemcpyFromSymbol(out48, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 48));
+  VAME_HIP(hipMemcpyFromSymbol(out96, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 96));
   if (reset) {
-    unsigned long long z[48] = {};
+    unsigned long long z[96] = {};
     VAME_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)));
   }
   return VAME_OK;

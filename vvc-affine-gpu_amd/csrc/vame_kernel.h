@@ -194,8 +194,9 @@ __device__ unsigned long long g_pred_count[20];
 #endif
 enum { kPhStage, kPhPredict, kPhCost, kPhGradient, kPhSolve, kPhTail, kNumPhases };
 #if VAME_PHASE_TIMING
-// [kernel: quad, ctu, half][phase + 6 for the 3-CP pass; 12, 13: SIMD-slot use]
-__device__ unsigned long long g_phase_cycles[3][16];
+// [kernel: quad, ctu, half, ctu2, half2w, half2h][phase + 6 for the 3-CP
+// pass; 12, 13: SIMD-slot use; 14: workgroups; 15: workgroup lifetimes]
+__device__ unsigned long long g_phase_cycles[6][16];
 #define PH_DECL unsigned long long ph_acc[2 * kNumPhases] = {}; unsigned long long ph_t = __builtin_amdgcn_s_memtime(); const unsigned long long ph_t0 = ph_t;
 #define PH_MARK(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_acc[(i) + ph_off] += t_ - ph_t; ph_t = t_; }
 // plus SIMD-slot use: [12] = waves x block lifetime, [13] = sum of wave lifetimes
@@ -211,6 +212,8 @@ __shared__ int s_ph_done;
     if (atomicAdd(&s_ph_done, 1) == nw_ - 1) { \
       atomicAdd(&g_phase_cycles[KIND][12], (unsigned long long)nw_ * (s_ph_blk[1] - s_ph_blk[0])); \
       atomicAdd(&g_phase_cycles[KIND][13], s_ph_blk[2]); \
+      atomicAdd(&g_phase_cycles[KIND][14], 1ull); \
+      atomicAdd(&g_phase_cycles[KIND][15], s_ph_blk[1] - s_ph_blk[0]); \
     } \
   } }
 #define PH_INIT { if (tid == 0) { s_ph_blk[0] = ~0ull; s_ph_blk[1] = 0; s_ph_blk[2] = 0; s_ph_done = 0; } }
