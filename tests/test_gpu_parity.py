@@ -368,6 +368,46 @@ def test_batch_equals_per_poc(engines):
                                           err_msg=f"POC{poc} ref{refidx} {name}")
 
 
+@pytest.mark.parametrize("env", [{"VAME_QUAD_ALT": "1"}, {"VAME_QUAD_ALT": "1", "VAME_JOIN_EACH": "1"},
+                                 {"VAME_STREAMS": "1"}, {"VAME_STREAMS": "4", "VAME_SYNC": "0"}],
+                         ids=["quad_kernels_alternating", "alternating_join_each", "one_stream",
+                              "four_streams_event_joins"])
+def test_batch_stream_variants(env, monkeypatch):
+    """A batch of two launches (42 pairs) under the multi-launch stream knobs
+    -- VAME_QUAD_ALT=1: the quadrant kernels alternate between two side
+    streams; VAME_JOIN_EACH=1: fork and join around every launch -- gives the
+    default context's results bit for bit."""
+    from vame import synth
+    from vame.engine import Engine
+    from vame.hostlogic import lambda_for_poc, ref_list
+    o, r = synth.synth_sequence(416, 240, 12, 32, seed=0xBA7D)
+
+    def run(eng):
+        jobs = [(dev(o[poc - 1]), [dev(r[k]) for k in ref_list(poc)], lambda_for_poc(32, poc),
+                 eng.alloc_poc(len(ref_list(poc)), 3)) for poc in range(1, 13)]
+        assert sum(len(j[1]) for j in jobs) > 32
+        outs = eng.affine_me_batch(jobs, 3, 0)
+        torch.cuda.synchronize()
+        return [{k: host(v) for k, v in out.items()} for out in outs]
+
+    base = Engine(416, 240, 0)
+    try:
+        want = run(base)
+    finally:
+        base.close()
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    eng = Engine(416, 240, 0)
+    try:
+        got = run(eng)
+    finally:
+        eng.close()
+    for poc, (g, w) in enumerate(zip(got, want), start=1):
+        for key in w:
+            np.testing.assert_array_equal(g[key][0], w[key][0], err_msg=f"POC{poc} {key}")
+            np.testing.assert_array_equal(g[key][1], w[key][1], err_msg=f"POC{poc} {key}")
+
+
 def test_calls_keep_the_current_device(engines):
     """The C-ABI entry points restore the caller's current device:
     two engines used from one thread leave torch.cuda.current_device() alone."""

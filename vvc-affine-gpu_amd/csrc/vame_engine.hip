@@ -94,6 +94,7 @@ struct vame_ctx {
   // capture (VAME_GRAPH): events.  syncWord[0] the fork, [1 + i] side stream
   // i's join.
   int valueSync = 1;
+  bool quadAlt = false;  // VAME_QUAD_ALT (see launch_direct)
   uint32_t* syncWord[4] = {nullptr, nullptr, nullptr, nullptr};
   uint32_t forkSeq = 0, joinSeq[3] = {0, 0, 0};
   // optional per-kernel timing: (start, end) event pairs per kernel class
@@ -585,6 +586,12 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
     sQuad = c->side[0];
     used[0] = true;
   }
+  // VAME_QUAD_ALT=1 (two-stream mode): a batch's quadrant kernels alternate
+  // between side streams 0 and 1, so launch k + 1's quadrant workgroups can
+  // fill the CUs that launch k's tail leaves idle (c3 / c4: within +-0.1 %,
+  // off by default)
+  const bool quadAlt = c->streams == 2 && c->quadAlt && used[0] && kps.size() > 1;
+  if (quadAlt) used[1] = true;
   if (c->streams > 2 && c->streams < 5 && anyHalf) {
     sHalf[0] = c->side[1];
     sHalf[1] = c->side[c->streams > 3 ? 2 : 1];
@@ -691,8 +698,9 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
     const unsigned grid = block_grid(c, 0, kq);
     hipEvent_t t0, t1;
     VAME_TRY(time_events(c, 0, t0, t1));
-    VAME_HIP(launch_kernel(kernel_for<kKindQuad>(c->prof, mode), grid, Cfg<kKindQuad>::THREADS, sQuad, t0, t1,
-                           order_flag(), kq, capture));
+    VAME_HIP(launch_kernel(kernel_for<kKindQuad>(c->prof, mode), grid, Cfg<kKindQuad>::THREADS,
+                           quadAlt && (&kp - kps.data()) % 2 ? c->side[1] : sQuad, t0, t1, order_flag(), kq,
+                           capture));
     return VAME_OK;
   };
   auto all = [&]() -> int {
@@ -890,6 +898,7 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming);
   c->valueSync = std::min(2, std::max(0, env_int("VAME_SYNC", 1)));
+  c->quadAlt = env_int("VAME_QUAD_ALT", 0) != 0;
   for (int i = 0; i < 4 && e == hipSuccess && c->valueSync; i++) {
     if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->syncWord[i]), 8, hipMallocSignalMemory) != hipSuccess ||
         hipMemset(c->syncWord[i], 0, 8) != hipSuccess) {
