@@ -95,6 +95,7 @@ struct vame_ctx {
   // i's join.
   int valueSync = 1;
   bool quadAlt = false;  // VAME_QUAD_ALT (see launch_direct)
+  bool halfFirst = false;  // VAME_HALF_FIRST=1: the 128x64 / 64x128 kernels before the 128x128 one
   uint32_t* syncWord[4] = {nullptr, nullptr, nullptr, nullptr};
   uint32_t forkSeq = 0, joinSeq[3] = {0, 0, 0};
   // optional per-kernel timing: (start, end) event pairs per kernel class
@@ -707,8 +708,9 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
     for (size_t k = 0; k < kps.size(); k++) {
       const bool quadFirst = c->streams == 1 && c->quadFirst;  // VAME_QUAD_FIRST (one-stream mode)
       if (quadFirst && (quadFull || quadHalf)) VAME_TRY(quad(kps[k]));
+      if (bigItems && use_half(kps[k]) && c->halfFirst) VAME_TRY(half(kps[k]));
       if (bigItems) VAME_TRY(big(kps[k]));
-      if (bigItems && use_half(kps[k])) VAME_TRY(half(kps[k]));
+      if (bigItems && use_half(kps[k]) && !c->halfFirst) VAME_TRY(half(kps[k]));
       if (!quadFirst && (quadFull || quadHalf)) VAME_TRY(quad(kps[k]));
       if (fork && (c->joinEach || k + 1 == kps.size())) {
         VAME_TRY(join_sides());
@@ -899,6 +901,7 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming);
   c->valueSync = std::min(2, std::max(0, env_int("VAME_SYNC", 1)));
   c->quadAlt = env_int("VAME_QUAD_ALT", 0) != 0;
+  c->halfFirst = env_int("VAME_HALF_FIRST", 0) != 0;
   for (int i = 0; i < 4 && e == hipSuccess && c->valueSync; i++) {
     if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->syncWord[i]), 8, hipMallocSignalMemory) != hipSuccess ||
         hipMemset(c->syncWord[i], 0, 8) != hipSuccess) {
