@@ -329,6 +329,11 @@ def main():
         # against the wave64 issue ceiling of 1,024 SIMDs at the peak clock
         "bound": "valu",
         "kernel": "affine_me_quad",
+        # the engine issues the 128-class kernels on the caller's stream and the
+        # quadrant kernel on a side stream (VAME_STREAMS=2): they run
+        # side by side, so this kernel's launch time includes their share of the
+        # GPU; step.valu_frac counts every kernel's instructions over the step
+        "concurrent_with": sorted(big_kernels) if os.environ.get("VAME_STREAMS", "2") != "1" else [],
         "achieved": roof_q.get("valu_Ginst_per_s"),
         "peak": VALU_PEAK_GINST,
         "unit": "G VALU wave-instructions/s",
