@@ -4,8 +4,8 @@ Runs a bench config's step through the profiling-only build
 `vvc-affine-gpu_amd/lib/libvame_phase.so` (`make phase`: every wave sums the
 shader clock per phase, vame_kernel.h VAME_PHASE_TIMING) and prints, per
 kernel class and pass, the share of wave cycles in each phase -- staging,
-prediction (+ SATD), cost, gradient + equation reduction, solve + CPMV update,
-results -- where a phase includes the wait at the barrier that ends it; the
+prediction (+ SATD), cost, gradient sums, equation reduction, solve + CPMV
+update, results -- where a phase includes the wait at the barrier that ends it; the
 SIMD-slot use (wave lifetimes / waves x workgroup lifetime) and the mean
 workgroup lifetime in cycles.  The counters cost ~10 % of wave cycles; the
 shares, not the times, are the result.
@@ -22,7 +22,9 @@ sys.path.insert(0, os.path.join(REPO, "vvc-affine-gpu_amd"))
 
 KINDS = ["affine_me_quad", "affine_me_ctu", "affine_me_half", "affine_me_ctu2", "affine_me_half2w",
          "affine_me_half2h"]
-PHASES = ["stage", "predict", "cost", "gradient", "solve", "tail"]
+PHASES = ["stage", "predict", "cost", "gradient", "solve", "tail", "reduce"]
+NP = len(PHASES)
+SLOTS = 2 * NP + 4
 
 
 def main():
@@ -40,7 +42,7 @@ def main():
     cfg = bench.CONFIGS[cfg_name]
     L = _lib.lib()
     L.vame_debug_phase_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    buf = (ctypes.c_ulonglong * 96)()
+    buf = (ctypes.c_ulonglong * (6 * SLOTS))()
     dev = torch.device("cuda", 0)
     n_pairs = sequence_pairs(cfg["frames"])
     eng = Engine(cfg["W"], cfg["H"], 0)
@@ -57,18 +59,19 @@ def main():
     out = {"config": cfg_name, "steps": steps, "env": {k: v for k, v in os.environ.items() if k.startswith("VAME_")},
            "kernels": {}}
     for k, name in enumerate(KINDS):
-        v = list(buf[16 * k:16 * k + 16])
-        total = sum(v[:12])
+        v = list(buf[SLOTS * k:SLOTS * k + SLOTS])
+        total = sum(v[:2 * NP])
         if not total:
             continue
         rec = {"wave_cycles": total}
         for p in range(2):
-            part = v[6 * p:6 * p + 6]
+            part = v[NP * p:NP * p + NP]
             if sum(part):
                 rec["pass%dcp" % (p + 2)] = {ph: round(c / total, 4) for ph, c in zip(PHASES, part)}
-        rec["simd_slot_use"] = round(v[13] / v[12], 4) if v[12] else None
-        rec["workgroups_per_step"] = v[14] / steps
-        rec["mean_wg_lifetime_cycles"] = round(v[15] / v[14]) if v[14] else None
+        w = 2 * NP
+        rec["simd_slot_use"] = round(v[w + 1] / v[w], 4) if v[w] else None
+        rec["workgroups_per_step"] = v[w + 2] / steps
+        rec["mean_wg_lifetime_cycles"] = round(v[w + 3] / v[w + 2]) if v[w + 2] else None
         out["kernels"][name] = rec
     print(json.dumps(out, indent=1))
 

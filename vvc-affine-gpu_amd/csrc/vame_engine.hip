@@ -1180,13 +1180,13 @@ const char* vame_last_hip_error(void) { return g_hip_err; }
 
 #if VAME_PHASE_TIMING
 // profiling-only builds: per-phase shader-clock sums [kernel: quad, ctu, half,
-// ctu2, half2w, half2h][pass phase ...] (see vame_kernel.h)
-int vame_debug_phase_cycles(unsigned long long* out96, int reset) {
-  if (!out96) return VAME_E_INVALID;
+// ctu2, half2w, half2h][kPhSlots] (see vame_kernel.h)
+int vame_debug_phase_cycles(unsigned long long* out, int reset) {
+  if (!out) return VAME_E_INVALID;
   VAME_HIP(hipDeviceSynchronize());
-  VAME_HIP(hipMemcpyFromSymbol(out96, HIP_SYMBOL(g_phase_cycles), sizeof(unsigned long long) * 96));
+  VAME_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(g_phase_cycles)));
   if (reset) {
-    unsigned long long z[96] = {};
+    unsigned long long z[6 * kPhSlots] = {};
     VAME_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof(z)));
   }
   return VAME_OK;

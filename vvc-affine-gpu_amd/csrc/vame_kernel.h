@@ -113,7 +113,8 @@ struct KParams {
 // bit 3 skip the prediction math, bit 4 skip the 128-class launch, bit 5 skip
 // the quadrant launch, bit 8 (host) 128-class templates without the 128x64 /
 // 64x128 items, bit 9 every 9x9 window read from the tile (no clamped-global path),
-// bit 10 the same in the 3-CP pass only.
+// bit 10 the same in the 3-CP pass only, bit 11 no seed-reuse sums stored by
+// the two-sub-block kernels' 2-CP pass.
 #ifndef VAME_ABLATE
 #define VAME_ABLATE 0
 #endif
@@ -124,6 +125,15 @@ struct KParams {
 // adds a workgroup barrier between the 2-CP and 3-CP passes of autonomous items.
 #ifndef VAME_DUP
 #define VAME_DUP 0
+#endif
+// SBL = 2: the original rows kept in registers from the prediction to the
+// gradient step instead of read again (VAME_OG_KEEP).
+#ifndef VAME_OG_KEEP
+#define VAME_OG_KEEP 0
+#endif
+// Non-temporal loads for the reference tile's staging (VAME_NT_TILE).
+#ifndef VAME_NT_TILE
+#define VAME_NT_TILE 0
 #endif
 // Wide, batched loads for windows outside the staged tile (filter_rows_global).
 #ifndef VAME_WIDE_GLOBAL
@@ -192,11 +202,14 @@ __device__ unsigned long long g_pred_count[20];
 #ifndef VAME_PHASE_TIMING
 #define VAME_PHASE_TIMING 0
 #endif
-enum { kPhStage, kPhPredict, kPhCost, kPhGradient, kPhSolve, kPhTail, kNumPhases };
+enum { kPhStage, kPhPredict, kPhCost, kPhGradient, kPhSolve, kPhTail, kPhReduce, kNumPhases };
 #if VAME_PHASE_TIMING
-// [kernel: quad, ctu, half, ctu2, half2w, half2h][phase + 6 for the 3-CP
-// pass; 12, 13: SIMD-slot use; 14: workgroups; 15: workgroup lifetimes]
-__device__ unsigned long long g_phase_cycles[6][16];
+// [kernel: quad, ctu, half, ctu2, half2w, half2h][phase + kNumPhases for the
+// 3-CP pass; then SIMD-slot use (2), workgroups, workgroup lifetimes]
+// (kPhGradient: the gradient sums; kPhReduce: the equations' reduction and
+// the barrier after it)
+constexpr int kPhSlots = 2 * kNumPhases + 4;
+__device__ unsigned long long g_phase_cycles[6][kPhSlots];
 #define PH_DECL unsigned long long ph_acc[2 * kNumPhases] = {}; unsigned long long ph_t = __builtin_amdgcn_s_memtime(); const unsigned long long ph_t0 = ph_t;
 #define PH_MARK(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_acc[(i) + ph_off] += t_ - ph_t; ph_t = t_; }
 // plus SIMD-slot use: [12] = waves x block lifetime, [13] = sum of wave lifetimes
@@ -210,10 +223,10 @@ __shared__ int s_ph_done;
     atomicAdd(&s_ph_blk[2], t1_ - ph_t0); \
     const int nw_ = (int)(blockDim.x >> 6); \
     if (atomicAdd(&s_ph_done, 1) == nw_ - 1) { \
-      atomicAdd(&g_phase_cycles[KIND][12], (unsigned long long)nw_ * (s_ph_blk[1] - s_ph_blk[0])); \
-      atomicAdd(&g_phase_cycles[KIND][13], s_ph_blk[2]); \
-      atomicAdd(&g_phase_cycles[KIND][14], 1ull); \
-      atomicAdd(&g_phase_cycles[KIND][15], s_ph_blk[1] - s_ph_blk[0]); \
+      atomicAdd(&g_phase_cycles[KIND][2 * kNumPhases], (unsigned long long)nw_ * (s_ph_blk[1] - s_ph_blk[0])); \
+      atomicAdd(&g_phase_cycles[KIND][2 * kNumPhases + 1], s_ph_blk[2]); \
+      atomicAdd(&g_phase_cycles[KIND][2 * kNumPhases + 2], 1ull); \
+      atomicAdd(&g_phase_cycles[KIND][2 * kNumPhases + 3], s_ph_blk[1] - s_ph_blk[0]); \
     } \
   } }
 #define PH_INIT { if (tid == 0) { s_ph_blk[0] = ~0ull; s_ph_blk[1] = 0; s_ph_blk[2] = 0; s_ph_done = 0; } }
@@ -1623,7 +1636,15 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         const int fy = clampi(ty0 + ty, 0, H - 1), fx = tx0 + cx;
         const uint16_t* row = ref + (size_t)fy * W;
         if (fx >= 0 && fx + 7 < W) {
+#if VAME_NT_TILE
+          // read once per item: a non-temporal load, so the reference rows do
+          // not push the CU's original samples (re-read every iteration) out of L2
+          typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + fx));
+          tv[j] = make_uint4(v.x, v.y, v.z, v.w);
+#else
           tv[j] = *reinterpret_cast<const uint4*>(row + fx);
+#endif
         } else {
           unsigned a[8];
 #pragma unroll
@@ -1976,7 +1997,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
                                      dpp32<0x130, 0xF>((int)Pr[j][r].x));
                 const uint2 nb = j + 1 < SBL ? Pr[j + 1][0] : bt;
                 X[5] = ext_row(nb, dpp32<0x138, 0xF>((int)nb.y), dpp32<0x130, 0xF>((int)nb.x));
-                {
+                if (!VAME_OG_KEEP) {
                   const unsigned b0 = (unsigned)((gg.y + syg + 4 * j) * W + gg.x + sxg) * 2u, bw = (unsigned)W * 2u;
                   const char* base = reinterpret_cast<const char*>(cur);
 #pragma unroll
@@ -1993,7 +2014,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
               grad_sb(sxd, syg, gg, X, Og[0], S2);
               asm volatile("" ::"v"(S2[0] ^ S2[1] ^ S2[2] ^ S2[3] ^ S2[4]));
             }
-            if (keepS && better) {  // the best iteration's sums, for the 3-CP seed reuse
+            if (keepS && better && !(SBL == 2 && (VAME_ABLATE & 2048))) {  // the best iteration's sums, for the 3-CP seed reuse
 #pragma unroll
               for (int j = 0; j < SBL; j++)
 #pragma unroll
@@ -2005,6 +2026,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
                 }
             }
           }
+          PH_MARK(kPhGradient)
           if (!(VAME_ABLATE & 4)) {
             long long* dst = s_val[myCu < 0 ? 0 : myCu];
             int va[SBL];
@@ -2025,7 +2047,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           }
         }
         phase_sync(coop);
-        PH_MARK(kPhGradient)
+        PH_MARK(kPhReduce)
 
         // =============== solve + CPMV update (affine.cl:782-893), per CU segment ===============
         __builtin_amdgcn_s_setprio(kSolvePrio);
