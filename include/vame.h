@@ -189,6 +189,13 @@ int vame_read_frames_range(const char* path, int width, int height, int first, i
  * the '\n' of [begin, end) (end < 0: to the end; ranks count disjoint chunks
  * and exchange the counts). */
 long long vame_count_lines(const char* path, long long begin, long long end, int nthreads);
+/* The '\n' counts of n byte ranges [begin[i], end[i]) of one file, into
+ * counts[i], in one pass over one mapping with one set of threads (a rank's
+ * chunks of a CSV: calling vame_count_lines per chunk paid a mapping and a
+ * thread start per 16 MB chunk).  Returns VAME_OK, or VAME_E_INVALID for a
+ * missing file, a negative or reversed range. */
+int vame_count_lines_ranges(const char* path, const long long* begin, const long long* end, int n,
+                            long long* counts, int nthreads);
 int vame_read_frames_span(const char* path, int width, int height, int first, int nframes,
                           long long span_begin, long long lines_before, long long span_end,
                           uint16_t* out, int nthreads);

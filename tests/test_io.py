@@ -396,6 +396,14 @@ def test_read_frames_span_from_chunk_index(tmp_path, K):
     bounds = [size * k // K for k in range(K + 1)]
     counts = [logs.count_lines(p, bounds[k], bounds[k + 1], nthreads=3) for k in range(K)]
     assert sum(counts) == logs.count_lines(p) == 6 * 240
+    # the batched form: every chunk at once, any subset, empty ranges, any order
+    assert logs.count_lines_ranges(p, [(bounds[k], bounds[k + 1]) for k in range(K)], nthreads=3) == counts
+    sub = list(range(K - 1, -1, -2))
+    assert logs.count_lines_ranges(p, [(bounds[k], bounds[k + 1]) for k in sub]) == [counts[k] for k in sub]
+    assert logs.count_lines_ranges(p, [(5, 5), (0, size), (size, size + 10)]) == [0, 6 * 240, 0]
+    assert logs.count_lines_ranges(p, []) == []
+    with pytest.raises(logs.VameError):
+        logs.count_lines_ranges(p, [(10, 5)])
     prefix = [0] + list(np.cumsum(counts))
     for first, n in ((0, 6), (0, 1), (2, 3), (5, 1), (3, 2)):
         span = logs.line_span(bounds, prefix, first * 240, (first + n) * 240)

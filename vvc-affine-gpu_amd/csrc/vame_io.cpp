@@ -632,6 +632,43 @@ long long vame_count_lines(const char* path, long long begin, long long end, int
   return c;
 }
 
+int vame_count_lines_ranges(const char* path, const long long* begin, const long long* end, int n,
+                            long long* counts, int nthreads) {
+  if (!path || n < 0 || (n > 0 && (!begin || !end || !counts))) return VAME_E_INVALID;
+  for (int i = 0; i < n; i++)
+    if (begin[i] < 0 || end[i] < begin[i]) return VAME_E_INVALID;
+  Mapped m;
+  if (int rc = map_file(path, m)) return rc;
+  // pieces of <= 4 MiB over all ranges, dealt to the threads in turn
+  constexpr size_t kPiece = size_t(4) << 20;
+  struct Piece {
+    int range;
+    size_t b, e;
+  };
+  std::vector<Piece> pieces;
+  for (int i = 0; i < n; i++) {
+    counts[i] = 0;
+    const size_t b = std::min((size_t)begin[i], m.n), e = std::min((size_t)end[i], m.n);
+    for (size_t o = b; o < e; o += kPiece) pieces.push_back({i, o, std::min(e, o + kPiece)});
+  }
+  std::vector<long long> per(pieces.size(), 0);
+  const int T = pick_threads(nthreads, (long)pieces.size());
+  parallel_for(T, (int)pieces.size(), [&](int k, int) {
+    const char* q = m.p + pieces[k].b;
+    const char* qe = m.p + pieces[k].e;
+    long long c = 0;
+    while (q < qe) {
+      const char* r = (const char*)memchr(q, '\n', (size_t)(qe - q));
+      if (!r) break;
+      c++;
+      q = r + 1;
+    }
+    per[k] = c;
+  });
+  for (size_t k = 0; k < pieces.size(); k++) counts[pieces[k].range] += per[k];
+  return VAME_OK;
+}
+
 int vame_read_frames_span(const char* path, int width, int height, int first_frame, int nframes,
                           long long span_begin, long long lines_before, long long span_end,
                           uint16_t* out, int nthreads) {

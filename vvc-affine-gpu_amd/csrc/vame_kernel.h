@@ -121,8 +121,7 @@ struct KParams {
 // VAME_DUP (timing-only builds, results stay correct): run a phase twice to
 // price it in throughput terms: bit 0 prediction, bit 1 gradient, bit 2
 // equation reduction, bit 6 the tile staging round trip, bit 4 the solve (on the system itself, before the real
-// one rebuilds it: no extra LDS); with bit 5 set, only in the 3-CP pass; bit 7
-// adds a workgroup barrier between the 2-CP and 3-CP passes of autonomous items.
+// one rebuilds it: no extra LDS); with bit 5 set, only in the 3-CP pass.
 #ifndef VAME_DUP
 #define VAME_DUP 0
 #endif
@@ -2168,9 +2167,6 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
       if constexpr (run3) run_pass(I3{}, T{}, F{});
     } else {
       if constexpr (run2) run_pass(I2{}, F{}, KeepS{});
-      if constexpr (run2 && run3 && (VAME_DUP & 128) != 0) {  // timing-only: a barrier between the passes
-        __syncthreads();
-      }
       if constexpr (run3) run_pass(I3{}, F{}, F{});
     }
     if (KIND != kKindQuad) break;  // 128-class items: one task

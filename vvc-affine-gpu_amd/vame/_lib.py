@@ -19,6 +19,7 @@ EXPORTS = (
     "vame_log_writer_refs", "vame_read_frames_range", "vame_count_lines", "vame_read_frames_span",
     "vame_log_writer_set_deferred", "vame_log_writer_num_files", "vame_log_writer_file_name",
     "vame_log_writer_sizes", "vame_log_writer_flush_at", "vame_template_coverage", "vame_pack_records",
+    "vame_count_lines_ranges",
 )
 
 
@@ -75,6 +76,7 @@ def lib():
         LL = ctypes.c_longlong
         L.vame_count_lines.argtypes = [C, LL, LL, I]
         L.vame_count_lines.restype = LL
+        L.vame_count_lines_ranges.argtypes = [C, P, P, I, P, I]
         L.vame_read_frames_span.argtypes = [C, I, I, I, I, LL, LL, LL, P, I]
         L.vame_log_remove_old.argtypes = [C]
         L.vame_log_write_headers.argtypes = [C, I]

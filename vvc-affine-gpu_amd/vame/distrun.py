@@ -442,15 +442,16 @@ def line_index(path: str, world: int, rank: int, dist, T: dict):
     K = max(world, min(64 * world, size >> 22))  # chunks of >= 4 MiB
     bounds = [size * k // K for k in range(K + 1)]
     counts = torch.zeros(K, dtype=torch.int64)
-    for k in range(rank, K, world):
-        counts[k] = logs.count_lines(path, bounds[k], bounds[k + 1])
+    mine = list(range(rank, K, world))  # one native pass over this rank's chunks
+    counts[mine] = torch.tensor(logs.count_lines_ranges(path, [(bounds[k], bounds[k + 1]) for k in mine]))
     if dist is not None:
         _all_reduce_cpu(dist, counts)
     else:
         t = time.perf_counter()
-        for k in range(K):
-            if k % world != rank:
-                counts[k] = logs.count_lines(path, bounds[k], bounds[k + 1])
+        others = [k for k in range(K) if k % world != rank]
+        if others:
+            counts[others] = torch.tensor(logs.count_lines_ranges(path, [(bounds[k], bounds[k + 1])
+                                                                         for k in others]))
         T["index_others_s"] = T.get("index_others_s", 0.0) + time.perf_counter() - t
     prefix = [0] + torch.cumsum(counts, 0).tolist()
     return bounds, prefix

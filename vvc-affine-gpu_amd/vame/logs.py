@@ -38,6 +38,20 @@ def count_lines(path: str, begin: int = 0, end: int = -1, nthreads: int = 0) -> 
     return n
 
 
+def count_lines_ranges(path: str, ranges, nthreads: int = 0) -> list[int]:
+    """'\\n' counts of several byte ranges [(begin, end), ...] of one file,
+    in one native pass (vame_count_lines_ranges)."""
+    b = np.ascontiguousarray([r[0] for r in ranges], dtype=np.int64)
+    e = np.ascontiguousarray([r[1] for r in ranges], dtype=np.int64)
+    out = np.zeros(len(ranges), dtype=np.int64)
+    rc = lib().vame_count_lines_ranges(path.encode(), b.ctypes.data_as(ctypes.c_void_p),
+                                       e.ctypes.data_as(ctypes.c_void_p), len(ranges),
+                                       out.ctypes.data_as(ctypes.c_void_p), nthreads)
+    if rc != 0:
+        raise VameError(f"cannot count the lines of {path} (rc={rc})")
+    return out.tolist()
+
+
 def line_span(bounds: list[int], prefix: list[int], line0: int, line1: int) -> tuple[int, int, int]:
     """(begin, lines_before, end) of the chunks that hold text lines [line0,
     line1), from chunk byte bounds[0..K] and prefix[k] = the newlines ahead of
