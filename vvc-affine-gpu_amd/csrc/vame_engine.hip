@@ -630,11 +630,8 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
       }
     return VAME_OK;
   };
-  for (int i = 1; i < 3; i++)
-    if (used[i] && !c->side[i]) {  // created on first use (vame_create)
-      VAME_HIP(hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking));
-      VAME_HIP(hipEventCreateWithFlags(&c->evJoin[i], hipEventDisableTiming));
-    }
+  for (int i = 0; i < 3; i++)
+    if (used[i] && !c->side[i]) return VAME_E_INVALID;  // (vame_create made the streams the knobs use)
   if (fork) VAME_TRY(fork_sides());
   auto big = [&](const KParams& kp) -> int {
     KParams kb = kp;
@@ -899,17 +896,22 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   if (e == hipSuccess && !hf.empty()) e = hipMalloc(&c->dHalf, hf.size() * sizeof(Item));
   if (e == hipSuccess && !hf.empty())
     e = hipMemcpy(c->dHalf, hf.data(), hf.size() * sizeof(Item), hipMemcpyHostToDevice);
-  // side stream 0 now; 1 and 2 on first use (launch_direct): a process has
+  c->valueSync = std::min(2, std::max(0, env_int("VAME_SYNC", 1)));
+  c->quadAlt = env_int("VAME_QUAD_ALT", 0) != 0;
+  c->halfFirst = env_int("VAME_HALF_FIRST", 0) != 0;
+  // only the side streams the knobs use (side stream 0 by default; 1 for
+  // VAME_STREAMS=3 / VAME_QUAD_ALT, 2 for VAME_STREAMS=4), created here, not
+  // during a launch (a launch may be under stream capture): a process has
   // GPU_MAX_HW_QUEUES = 4 hardware queues and HIP shares them between its
   // streams beyond that, so an idle stream created here could put the
   // caller's own copy streams on the quadrant kernel's queue (the CLI's
   // compute, upload and download streams + side stream 0 are four)
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side[0], hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin[0], hipEventDisableTiming);
+  const int nSide = c->streams == 4 ? 3 : (c->streams == 3 || (c->streams == 2 && c->quadAlt)) ? 2 : 1;
+  for (int i = 0; i < nSide && e == hipSuccess; i++) {
+    e = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin[i], hipEventDisableTiming);
+  }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming);
-  c->valueSync = std::min(2, std::max(0, env_int("VAME_SYNC", 1)));
-  c->quadAlt = env_int("VAME_QUAD_ALT", 0) != 0;
-  c->halfFirst = env_int("VAME_HALF_FIRST", 0) != 0;
   for (int i = 0; i < 4 && e == hipSuccess && c->valueSync; i++) {
     if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->syncWord[i]), 8, hipMallocSignalMemory) != hipSuccess ||
         hipMemset(c->syncWord[i], 0, 8) != hipSuccess) {
