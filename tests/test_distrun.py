@@ -152,11 +152,12 @@ def test_launch_batches_and_cuts():
     batches = distrun.launch_batches(blocks)
     assert [e for b in batches for e in b] == blocks
     assert all(sum(len(r) for _, r in b) <= distrun.MAX_PAIRS for b in batches)
-    # a small first launch (the GPU starts once its frames are parsed), then full ones
+    # a small first launch (the GPU starts once its frames are parsed), doubling up to full ones
     small = distrun.launch_batches(blocks, 8)
     assert [e for b in small for e in b] == blocks
-    assert sum(len(r) for _, r in small[0]) <= 8
-    assert all(sum(len(r) for _, r in b) <= distrun.MAX_PAIRS for b in small[1:])
+    sizes = [sum(len(r) for _, r in b) for b in small]
+    assert sizes[0] <= 8 and sizes[1] <= 16 and sizes[2] <= 32 and sizes[1] > 8
+    assert all(s <= distrun.MAX_PAIRS for s in sizes) and max(sizes) > 16
     # the 6-POC sequence over 2 / 3 ranks cuts POC 4 / POC 5 between ranks
     for world, cut in ((2, [4]), (3, [5])):
         owners = {}

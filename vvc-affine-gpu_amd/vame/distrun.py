@@ -101,11 +101,12 @@ def part_prefix(prefix: str, rank: int) -> str:
 
 def launch_batches(blocks, first: int = MAX_PAIRS):
     """The block's entries in launches of at most MAX_PAIRS pairs (entries
-    whole); the first launch holds at most `first` pairs (the GPU starts once
-    its few frames are parsed, while the rest are parsed behind it)."""
+    whole); the first launches ramp up from `first` pairs, doubling (the GPU
+    starts once the first launch's few frames are parsed, and each launch's
+    kernels cover the parsing of the next, larger one's frames)."""
     out, cur, n = [], [], 0
     for poc, refs in blocks:
-        if cur and n + len(refs) > (first if not out else MAX_PAIRS):
+        if cur and n + len(refs) > min(MAX_PAIRS, first << len(out)):
             out.append(cur)
             cur, n = [], 0
         cur.append((poc, refs))
