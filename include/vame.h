@@ -63,15 +63,28 @@ typedef struct {
 
 /* Create a context on HIP device `device` for frames of width x height (one of
  * the reference's resolutions: constants.h:73-79 / main.cpp:257-265).
- * Tuning knobs read here (results are bit-identical under every setting; the
- * defaults are the measured best on MI355X): work packing
- * VAME_TASKS (wave tasks per autonomous quadrant item, 1..16, default 16),
- * VAME_CLAIM, VAME_CHAIN, VAME_MIX (default 1 each), VAME_HALF128, VAME_CTU2,
- * VAME_HALF2, VAME_HALF_MIN_PAIRS; launch structure VAME_STREAMS, VAME_QUAD_FIRST,
- * VAME_GRAPH, VAME_JOIN_EACH; block order VAME_ITEM_ORDER, VAME_XCD_ORDER, VAME_GROUP_COMBOS,
- * VAME_GROUP_COMBOS_BIG. */
+ * Every device buffer the launches use is allocated here (the reference
+ * allocates its buffers before the POC loop, main.cpp:473-552), among them the
+ * 3-CP seed-reuse scratch for 32 pairs per launch (~1 GB at 3840x2160; see
+ * vame_set_max_pairs): no launch allocates, so a call may be captured into a
+ * hipGraph on the caller's stream.  Runtime knobs, read here (results are
+ * bit-identical under every setting; the defaults are the measured best on
+ * MI355X):
+ *   VAME_STREAMS       2 (default): the quadrant kernel on a side stream of the
+ *                      context, forked from and joined into the caller's stream;
+ *                      1: every kernel on the caller's stream
+ *   VAME_SYNC          1 (default): the join as a stream memory operation;
+ *                      0: an event
+ *   VAME_GROUP_COMBOS  (CTU, pair) combinations per block-order group (408) */
 int vame_create(vame_ctx** out, int device, int width, int height);
 void vame_destroy(vame_ctx* ctx);
+/* (POC, refIdx) pairs per launch of the fused calls, 1..32 (default 32): the
+ * seed-reuse scratch is re-sized for it (synchronizes the device; outside any
+ * capture), batches are cut into launches of at most that many pairs.  A
+ * caller coding a few pairs per call (the CLI: one POC, <= 4 pairs) keeps the
+ * scratch at 1/8 of the default.  vame_get_max_pairs returns the setting. */
+int vame_set_max_pairs(vame_ctx* ctx, int max_pairs);
+int vame_get_max_pairs(vame_ctx* ctx);
 
 /* One reference launch (affine.cl:11 or :960 built with -DnCP=nCP).
  *   ref, cur : W*H uint16 samples (10-bit), device memory
@@ -92,7 +105,8 @@ int vame_affine_me_poc(vame_ctx* ctx, const uint16_t* cur, const uint16_t* const
                        const vame_poc_result* out, void* stream);
 
 /* Batched fused call: several POCs (each one vame_affine_me_poc) in as few
- * launches as possible (32 (POC, refIdx) pairs per launch), so consecutive
+ * launches as possible (vame_get_max_pairs() (POC, refIdx) pairs per launch,
+ * default 32), so consecutive
  * POCs share one grid -- no launch gaps or tails between them.  Results are
  * identical to one vame_affine_me_poc per job. */
 typedef struct {
@@ -128,30 +142,29 @@ int vame_set_prof(vame_ctx* ctx, int enable);
 /* Device-side kernel timing (the reference's per-PRED kernelExecutionTime,
  * main.cpp:856-866): when enabled, every kernel launch carries hipEvents in its
  * own dispatch on the stream it runs on.  kernel_class 0 = quadrant work items
- * (affine_me_quad); 1 = CTU items (affine_me_ctu: every 128-class CU in launches
- * of fewer than VAME_HALF_MIN_PAIRS pairs); 2 = single 128x64 / 64x128 CUs
- * (affine_me_half, with VAME_HALF2=0), 3 = single 128x128 CUs
- * (affine_me_ctu2), 4 / 5 = single 128x64 / 64x128 CUs (affine_me_half2w /
- * _half2h): 2 / 4 / 5 and 3 in launches of at least VAME_HALF_MIN_PAIRS pairs
- * (VAME_HALF128 / VAME_CTU2 / VAME_HALF2 select the other packings).
+ * (affine_me_quad); 3 = the 128x128 CUs (affine_me_ctu2); 4 / 5 = the 128x64 /
+ * 64x128 CUs (affine_me_half2w / _half2h); under PROF 1 = the 128x128 CUs
+ * (affine_me_ctu_prof), 2 = the 128x64 / 64x128 CUs (affine_me_half_prof).
  * enable = 2 times the quadrant kernel only (its dispatches carry the events;
  * the 128-class launches run untimed).  vame_get_timing waits for the recorded
  * launches and returns their summed duration and count since the last reset.
  * enable | VAME_TIMING_KEEP changes what later launches record without
- * dropping the launches recorded so far (timing a sample of a run's steps). */
+ * dropping the launches recorded so far (timing a sample of a run's steps).
+ * Launches on a stream under capture carry no events. */
 enum { VAME_TIMING_KEEP = 16 };
 int vame_set_timing(vame_ctx* ctx, int enable);
 int vame_get_timing(vame_ctx* ctx, int kernel_class, double* total_ms, int* launches, int reset);
 
 /* Work-item templates (no device work): how many times the engine's work
  * items -- quadrant, 128x128 and 128x64 / 64x128 items, as vame_create builds
- * them; half128 != 0: the affine_me_half packing, 0: the CTU packing -- cover each of the CTU's
- * candidate CUs of `align`: hits[0 .. {201|284}) indexed by the output offset
- * RETURN_STRIDE[group] + cuIdx (affine.cl:936 / :1929).  A valid partition
- * covers every CU exactly once (the quadrant items of one-alignment launches;
- * VAME_E_INVALID if those of both-alignment launches cover differently).
- * Also returns the item counts per kernel class (quad -- of a both-alignment
- * launch --, ctu, half) in items3 when non-NULL. */
+ * them -- cover each of the CTU's candidate CUs of `align`: hits[0 ..
+ * {201|284}) indexed by the output offset RETURN_STRIDE[group] + cuIdx
+ * (affine.cl:936 / :1929).  A valid partition covers every CU exactly once
+ * (the quadrant items of one-alignment launches; VAME_E_INVALID if those of
+ * both-alignment launches cover differently).  half128 must be non-zero (the
+ * one packing: every 128x64 / 64x128 CU a work item of its own).  Also returns
+ * the item counts per kernel class (quad -- of a both-alignment launch --,
+ * 128x128, 128x64 + 64x128) in items3 when non-NULL. */
 int vame_template_coverage(int half128, int align, int32_t* hits, int32_t* items3);
 
 /* Geometry / host helpers (no device work). */

@@ -95,6 +95,7 @@ def test_cli_logs_byte_identical_416(seq416):
     assert abs(sum(preds) - t["FUSED_POC_EXEC"]) <= 1e-3 * t["FUSED_POC_EXEC"] + 4
     assert t["TOTAL_EXEC_TIME(6x)"] == t["FUSED_POC_EXEC"]
     assert preds[0] > preds[1] and preds[2] > preds[3]  # 6 vs 5 predictions per iteration set
+    assert "PRED_EXEC_SOURCE,estimated-apportioned" in stdout.splitlines()  # named as estimates
 
 
 def test_cli_per_launch_and_two_workers_identical(seq416):
@@ -107,6 +108,11 @@ def test_cli_per_launch_and_two_workers_identical(seq416):
          if l.endswith(tuple("0123456789")) and "_EXEC," in l}
     assert all(t[k] > 0 for k in ("FULL_2CP_EXEC", "FULL_3CP_EXEC", "HALF_2CP_EXEC",
                                   "HALF_3CP_EXEC"))
+    # per launch the keys are the launches' own event times, summing to TOTAL_EXEC_TIME
+    assert "PRED_EXEC_SOURCE,measured" in stdout.splitlines()
+    total = [float(l.split(",")[1]) for l in stdout.splitlines() if l.startswith("TOTAL_EXEC_TIME(")][0]
+    assert abs(sum(t[k] for k in ("FULL_2CP_EXEC", "FULL_3CP_EXEC", "HALF_2CP_EXEC", "HALF_3CP_EXEC"))
+               - total) <= 0.02 * total
     out2, _ = run_cli(tmp, 416, 240, 6, 32, ["--devices", "0,0", "--threads", "3"],
                       name="two_workers")
     compare_dirs(out2, exp)

@@ -134,11 +134,12 @@ def test_alignment_selection(engines, modes):
 REF_HARNESS = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle", "_ref", "ref_harness_hip")
 
 
-def run_reference(tmp_path, W, H, lam, ref, cur, tag, extra=0):
+def run_reference(tmp_path, W, H, lam, ref, cur, tag, extra=0, names=tuple(MODES)):
     """The reference kernels themselves (oracle/_ref: affine.cl compiled
-    unmodified for gfx950, the host's four launches replayed by
-    ref_harness_hip, ExtraGradientIter = `extra`) on one (POC, ref) pair, run
-    twice (A/B).  Returns the two runs' {PRED: (cost, cpmv[n, 6])}."""
+    unmodified for gfx950, the host's launches replayed by ref_harness_hip,
+    ExtraGradientIter = `extra`; `names`: the PREDs launched, REF_PRED_MASK)
+    on one (POC, ref) pair, run twice (A/B).  Returns the two runs' {PRED:
+    (cost, cpmv[n, 6])}."""
     d = os.path.dirname(REF_HARNESS)
     nctu = {(3840, 2160): 510, (1920, 1080): 135}[(W, H)]
     ref.tofile(tmp_path / f"{tag}_ref.u16")
@@ -148,10 +149,12 @@ def run_reference(tmp_path, W, H, lam, ref, cur, tag, extra=0):
         out = tmp_path / f"{tag}_{ab}"
         (tmp_path / f"{tag}_jobs_{ab}.txt").write_text(
             f"{W} {H} {lam!r} {extra} {tmp_path / (tag + '_ref.u16')} {tmp_path / (tag + '_cur.u16')} {out}\n")
+        mask = sum(1 << list(MODES).index(n) for n in names)
         subprocess.run([REF_HARNESS, os.path.join(d, "affine_2cp.co"), os.path.join(d, "affine_3cp.co"),
-                        str(tmp_path / f"{tag}_jobs_{ab}.txt")], check=True, timeout=300, capture_output=True)
+                        str(tmp_path / f"{tag}_jobs_{ab}.txt")], check=True, timeout=300, capture_output=True,
+                       env=dict(os.environ, REF_PRED_MASK=str(mask)))
         res = {}
-        for name in MODES:
+        for name in names:
             n = nctu * (201 if name.startswith("FULL") else 284)
             raw = np.fromfile(f"{out}_{name}.bin", np.uint8)
             res[name] = (raw[:n * 8].view(np.int64), raw[n * 8:].view(np.int32).reshape(n, 7)[:, 1:])
@@ -167,18 +170,20 @@ def check_vs_live_reference(runs, out, key_of, ref, cur, lam, extra=0):
     (as in the golden pipeline, make_golden.py pack); if they do not, the HIP
     path is checked against the oracle instead and the test reports the
     reference-side race as an xfail."""
-    racy = [name for name in MODES if not (np.array_equal(runs[0][name][0], runs[1][name][0])
+    names = list(runs[0])
+    racy = [name for name in names if not (np.array_equal(runs[0][name][0], runs[1][name][0])
                                            and np.array_equal(runs[0][name][1], runs[1][name][1]))]
     if racy:
         want = O.affine_me_pair(ref, cur, lam, extra)
-        for name, key in MODES.items():
+        for name in names:
+            key = MODES[name]
             hc, hp = host(out[key_of(name)])
             oc, op = want[key]
             np.testing.assert_array_equal(hc, oc, err_msg=name)
             np.testing.assert_array_equal(cp6(hp), oracle_cp6(op), err_msg=name)
         pytest.xfail(f"reference runs disagree (its global-memory race, affine.cl:487-514 / "
                      f"715-738) on {racy}; the HIP path equals the oracle")
-    for name in MODES:
+    for name in names:
         cost, cp = runs[0][name]
         hc, hp = host(out[key_of(name)])
         np.testing.assert_array_equal(hc, cost, err_msg=name)
@@ -239,26 +244,34 @@ def test_live_reference_configs(engines, tmp_path, W, H, qp, poc, refidx, extra)
     job = (dev(orig[poc]), d_refs, lam, eng.alloc_poc(len(refs), 3))
     eng.affine_me_batch([job], 3, extra)
     check_vs_live_reference(runs, job[3], lambda name: (refidx, name), recon[rp], orig[poc], lam, extra)
-    # both packings of the 128-class CUs: the default (affine_me_ctu2 and
-    # affine_me_half2w / _half2h) ran above; the 1024-thread CTU items here
-    from vame.engine import Engine
-    knobs = {"VAME_HALF128": "0", "VAME_CTU2": "0"}
-    old = {k: os.environ.get(k) for k in knobs}
-    os.environ.update(knobs)
-    try:
-        eng_half = Engine(W, H, 0)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
-    try:
-        job_h = (job[0], d_refs, lam, eng_half.alloc_poc(len(refs), 3))
-        eng_half.affine_me_batch([job_h], 3, extra)
-        check_vs_live_reference(runs, job_h[3], lambda name: (refidx, name), recon[rp], orig[poc], lam, extra)
-    finally:
-        eng_half.close()
+
+
+@pytest.mark.skipif(not os.path.exists(REF_HARNESS), reason="reference kernels not built")
+@pytest.mark.timeout(300)
+def test_live_reference_c2_step_2cp_only(engines, tmp_path):
+    """the benchmarked kernels themselves -- the 2-CP-only
+    instantiations (MODE 1: affine_me_quad<1>, affine_me_ctu2<1>,
+    affine_me_half2w<1> / _half2h<1>) -- against the reference kernels built
+    with -DnCP=2 (affine.cl:11 / :960, main.cpp:389-392), launched as
+    FULL_2CP + HALF_2CP only (REF_PRED_MASK = 5): the c2 step exactly as
+    bench.py codes it (1920x1080 QP32, POCs 1 and 2 of the bench's sequence in
+    one vame_affine_me_batch call, modes = 1), each of its three pairs, every
+    cost and CPMV component, bit for bit."""
+    from vame import synth
+    from vame.hostlogic import lambda_for_poc, ref_list
+    W, H, qp = 1920, 1080, 32
+    orig, recon = synth.synth_pocs(W, H, [1, 2], sorted({p for q in (1, 2) for p in ref_list(q)}), qp)
+    eng = engines(W, H)
+    jobs = [(dev(orig[poc]), [dev(recon[p]) for p in ref_list(poc)], lambda_for_poc(qp, poc),
+             eng.alloc_poc(len(ref_list(poc)), 1)) for poc in (1, 2)]
+    eng.affine_me_batch(jobs, 1, 0)
+    for poc, job in zip((1, 2), jobs):
+        assert set(k[1] for k in job[3]) == {"FULL_2CP", "HALF_2CP"}
+        for refidx, rp in enumerate(ref_list(poc)):
+            lam = lambda_for_poc(qp, poc)
+            runs = run_reference(tmp_path, W, H, lam, recon[rp], orig[poc], f"c2p{poc}r{refidx}",
+                                 names=("FULL_2CP", "HALF_2CP"))
+            check_vs_live_reference(runs, job[3], lambda name, r=refidx: (r, name), recon[rp], orig[poc], lam)
 
 
 PROF_CASES = [p for p in GOLDEN if any(k in p for k in ("qp32_poc1", "bigmotion", "extra1", "s832"))]
@@ -368,14 +381,14 @@ def test_batch_equals_per_poc(engines):
                                           err_msg=f"POC{poc} ref{refidx} {name}")
 
 
-@pytest.mark.parametrize("env", [{"VAME_QUAD_ALT": "1"}, {"VAME_QUAD_ALT": "1", "VAME_JOIN_EACH": "1"},
-                                 {"VAME_STREAMS": "1"}, {"VAME_STREAMS": "4", "VAME_SYNC": "0"}],
-                         ids=["quad_kernels_alternating", "alternating_join_each", "one_stream",
-                              "four_streams_event_joins"])
-def test_batch_stream_variants(env, monkeypatch):
-    """A batch of two launches (42 pairs) under the multi-launch stream knobs
-    -- VAME_QUAD_ALT=1: the quadrant kernels alternate between two side
-    streams; VAME_JOIN_EACH=1: fork and join around every launch -- gives the
+@pytest.mark.parametrize("env,max_pairs", [({"VAME_STREAMS": "1"}, 32), ({"VAME_SYNC": "0"}, 32), ({}, 5),
+                                           ({"VAME_STREAMS": "1"}, 1)],
+                         ids=["one_stream", "event_joins", "launches_of_5_pairs", "one_stream_launches_of_1_pair"])
+def test_batch_stream_variants(env, max_pairs, monkeypatch):
+    """A batch of 42 pairs under the launch-structure knobs (VAME_STREAMS=1:
+    every kernel on the caller's stream; VAME_SYNC=0: the join as an event)
+    and cut into launches of fewer pairs (vame_set_max_pairs: the seed-reuse
+    scratch re-sized, 9 / 42 launches forked once and joined once) gives the
     default context's results bit for bit."""
     from vame import synth
     from vame.engine import Engine
@@ -399,6 +412,8 @@ def test_batch_stream_variants(env, monkeypatch):
         monkeypatch.setenv(k, v)
     eng = Engine(416, 240, 0)
     try:
+        eng.set_max_pairs(max_pairs)
+        assert eng.max_pairs == max_pairs
         got = run(eng)
     finally:
         eng.close()
@@ -475,50 +490,19 @@ def test_property_translation_1080p(engines, d):
     assert n > 1000 and frac >= 0.75, (frac, n)
 
 
-@pytest.mark.parametrize("env", [{"VAME_HALF128": "0", "VAME_CTU2": "0"}, {"VAME_HALF128": "0"},
-                                 {"VAME_HALF128": "2", "VAME_CTU2": "1"}, {"VAME_CTU2": "0"},
-                                 {"VAME_HALF2": "0"}, {"VAME_STREAMS": "1"},
-                                 {"VAME_STREAMS": "1", "VAME_QUAD_FIRST": "0"}, {"VAME_STREAMS": "3"},
-                                 {"VAME_STREAMS": "4"}, {"VAME_STREAMS": "5"}, {"VAME_SYNC": "0"}, {"VAME_SYNC": "2"},
-                                 {"VAME_STREAMS": "4", "VAME_SYNC": "2", "VAME_JOIN_EACH": "1"},
-                                 {"VAME_GRAPH": "1"}, {"VAME_GRAPH": "1", "VAME_STREAMS": "4"},
-                                 {"VAME_GRAPH": "1", "VAME_STREAMS": "1", "VAME_HALF128": "0", "VAME_CTU2": "0"},
-                                 {"VAME_MIX": "0"}, {"VAME_TASKS": "8"},
-                                 {"VAME_TASKS": "4", "VAME_CHAIN": "0", "VAME_MIX": "0"}, {"VAME_TASKS": "1"},
-                                 {"VAME_CLAIM": "0"}, {"VAME_ITEM_ORDER": "0"}],
-                         ids=["ctu1024_items", "ctu2_and_ctu1024_items", "packing_by_launch_size", "ctu1024_128x128",
-                              "half512_one_sb_per_lane", "one_stream", "one_stream_128_class_first",
-                              "three_streams", "four_streams", "128_class_on_side_stream", "event_joins",
-                              "value_fork_and_joins", "four_streams_value_sync_join_each", "graph",
-                              "graph_four_streams", "graph_one_stream_ctu1024_items", "aligns_unmixed",
-                              "items_of_8", "items_of_4_unchained_unmixed", "items_of_1_task",
-                              "static_tasks", "items_by_quadrant"])
+@pytest.mark.parametrize("env", [{"VAME_STREAMS": "1"}, {"VAME_SYNC": "0"}, {"VAME_STREAMS": "1", "VAME_SYNC": "0"}],
+                         ids=["one_stream", "event_joins", "one_stream_no_words"])
 def test_launch_structure_variants(env, monkeypatch):
     """The engine's launch-structure knobs (read at vame_create) change only
     where the work runs (defaults: the 128x128 CUs in affine_me_ctu2, every
     128x64 / 64x128 CU in an affine_me_half2w / _half2h workgroup of its own,
-    the quadrant kernel on a side stream, the joins as stream memory
-    operations): VAME_HALF128=0 keeps the 128x64 / 64x128 CUs in 1024-thread
-    CTU items (2: by launch size), VAME_CTU2=0 runs the 128x128 CUs in them
-    too (1: by launch size); VAME_HALF2=0 runs the half packing in
-    affine_me_half (512 threads, one sub-block per lane); VAME_STREAMS=1
-    issues every kernel on the caller's stream (all but the first without the
-    AQL barrier bit; VAME_QUAD_FIRST=0: the 128-class kernels first), 3 / 4
-    give the 128x64 / 64x128 kernels side streams of their own, 5 puts the
-    128-class kernels on the side stream and the quadrant kernel on the
-    caller's; VAME_SYNC=0 joins with events, 2 forks by a stream memory
-    operation too (VAME_JOIN_EACH=1: fork and join around every launch);
-    VAME_TASKS=8 / 4 / 1 packs 8 / 4 / 1 wave tasks per autonomous quadrant
-    item (default 16 over the one staged tile, each wave claiming the next
-    task as it finishes; VAME_CLAIM=0: wave w runs tasks w, w + 4, ...),
-    VAME_CHAIN=0 gives each cooperative group an item of its own instead of
-    one chained cooperative item per quadrant, VAME_MIX=0 runs a launch of
-    both alignments on the two alignments' own items, VAME_ITEM_ORDER=0 lists
-    the autonomous items quadrant by quadrant; VAME_GRAPH=1 captures a call's launches
-    into a hipGraph and replays it when the call repeats (each call below runs
-    twice, the second from the graph, after its outputs were cleared).  A 1080p
-    POC with 2 refs (2+3 CP) and a 2-CP-only POC give the default context's
-    results bit for bit, and the default equals the oracle on one pair."""
+    on the caller's stream, the quadrant kernel on a side stream, the join as
+    a stream memory operation): VAME_STREAMS=1 issues every kernel on the
+    caller's stream (the quadrant kernel first, the others without the AQL
+    barrier bit), VAME_SYNC=0 joins with an event.  A 1080p POC with 2 refs
+    (2+3 CP) and a 2-CP-only POC give the default context's results bit for
+    bit (each call runs twice, the second after its outputs were cleared), and
+    the default equals the oracle on one pair."""
     from vame.engine import Engine
     from vame import synth
     o, r = synth.synth_sequence(1920, 1080, 2, 32, seed=0x0DE6)
@@ -533,7 +517,7 @@ def test_launch_structure_variants(env, monkeypatch):
         out = eng.alloc_poc(2, m)
         eng.affine_me_poc(cur, refs, 70.335619, modes=m, out=out)
         torch.cuda.synchronize()
-        for c, p in out.values():  # the repeat (a graph replay under VAME_GRAPH) must rewrite them
+        for c, p in out.values():  # the repeat must rewrite them
             c.fill_(-1)
             p.fill_(-1)
         eng.affine_me_poc(cur, refs, 70.335619, modes=m, out=out)
@@ -551,11 +535,11 @@ def test_launch_structure_variants(env, monkeypatch):
     base.close()
 
 
-@pytest.mark.parametrize("combos,order", [(16, 0), (24, 1), (64, 2), (408, 4), (100, 3)])
-def test_block_order_variants(combos, order, monkeypatch):
-    """The block order's knobs (VAME_GROUP_COMBOS / _BIG, VAME_XCD_ORDER, read
-    at vame_create: CTU chunks, XCD dealing) only move work between XCDs: a
-    1080p POC with 2 refs gives the default context's results bit for bit."""
+@pytest.mark.parametrize("combos", [16, 24, 64, 100])
+def test_block_order_variants(combos, monkeypatch):
+    """The block order's knob (VAME_GROUP_COMBOS, read at vame_create: CTU
+    chunks per group) only moves work between XCDs: a 1080p POC with 2 refs
+    gives the default context's results bit for bit."""
     from vame.engine import Engine
     from vame import synth
     o, r = synth.synth_sequence(1920, 1080, 2, 32, seed=0x0DE5)
@@ -563,8 +547,6 @@ def test_block_order_variants(combos, order, monkeypatch):
     base = Engine(1920, 1080, 0)
     want = base.affine_me_poc(cur, refs, 70.335619, modes=3)
     monkeypatch.setenv("VAME_GROUP_COMBOS", str(combos))
-    monkeypatch.setenv("VAME_GROUP_COMBOS_BIG", str(max(8, combos // 2)))
-    monkeypatch.setenv("VAME_XCD_ORDER", str(order))
     eng = Engine(1920, 1080, 0)
     got = eng.affine_me_poc(cur, refs, 70.335619, modes=3)
     torch.cuda.synchronize()
@@ -572,6 +554,81 @@ def test_block_order_variants(combos, order, monkeypatch):
         assert torch.equal(want[k][0], got[k][0]) and torch.equal(want[k][1], got[k][1]), k
     eng.close()
     base.close()
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("env", [{}, {"VAME_STREAMS": "1"}], ids=["default", "one_stream"])
+def test_first_call_captured_into_graph(env, monkeypatch):
+    """VERDICT r5 item 3 / ADVICE r5: a fresh context's FIRST 2+3-CP call
+    captured into a graph on a user stream (torch.cuda.graph) -- no device
+    allocation inside the capture (the seed-reuse scratch comes with
+    vame_create), the fork / join as graph edges (no stream memory operations
+    under capture) -- then replayed twice after its outputs were cleared: the
+    replays equal a direct call, and the caller's stream waits for every
+    kernel of the replay (results read right after replay + synchronize)."""
+    from vame.engine import Engine
+    from vame import synth
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    o, r = synth.synth_sequence(1920, 1080, 2, 32, seed=0x0DE7)
+    cur, refs = dev(o[1]), [dev(r[1]), dev(r[0])]
+    eng = Engine(1920, 1080, 0)
+    direct = Engine(1920, 1080, 0)
+    try:
+        out = eng.alloc_poc(2, 3)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            eng.affine_me_poc(cur, refs, 70.335619, modes=3, out=out)
+        want = direct.affine_me_poc(cur, refs, 70.335619, modes=3)
+        for _ in range(2):
+            for c, p in out.values():
+                c.fill_(-1)
+                p.fill_(-1)
+            g.replay()
+            torch.cuda.synchronize()
+            for k in want:
+                assert torch.equal(want[k][0], out[k][0]) and torch.equal(want[k][1], out[k][1]), k
+        # the same context still launches directly after the capture
+        again = eng.affine_me_poc(cur, refs, 70.335619, modes=3)
+        torch.cuda.synchronize()
+        for k in want:
+            assert torch.equal(want[k][0], again[k][0]) and torch.equal(want[k][1], again[k][1]), k
+        del g
+    finally:
+        eng.close()
+        direct.close()
+
+
+@pytest.mark.timeout(200)
+def test_calls_on_two_streams_share_the_scratch():
+    """the seed-reuse scratch is one buffer per context; two 2+3-CP
+    calls issued back to back on two different streams (one host thread) must
+    not overlap on it: the second call's stream waits for the first call.
+    Each result equals a call on a context of its own."""
+    from vame.engine import Engine
+    from vame import synth
+    o, r = synth.synth_sequence(1920, 1080, 3, 32, seed=0x0DE8)
+    jobs = [(dev(o[1]), [dev(r[1]), dev(r[0])], 70.335619), (dev(o[2]), [dev(r[2]), dev(r[1])], 78.949063)]
+    eng = Engine(1920, 1080, 0)
+    ref_eng = Engine(1920, 1080, 0)
+    try:
+        want = [ref_eng.affine_me_poc(c, rs, lam, modes=3) for c, rs, lam in jobs]
+        torch.cuda.synchronize()
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        got = []
+        for _ in range(3):
+            got = []
+            for (c, rs, lam), s in zip(jobs, streams):
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    got.append(eng.affine_me_poc(c, rs, lam, modes=3))
+            torch.cuda.synchronize()
+            for w, g_ in zip(want, got):
+                for k in w:
+                    assert torch.equal(w[k][0], g_[k][0]) and torch.equal(w[k][1], g_[k][1]), k
+    finally:
+        eng.close()
+        ref_eng.close()
 
 
 PROBE = os.path.join(os.path.dirname(__file__), "native", "anyorder_probe")

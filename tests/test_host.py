@@ -47,34 +47,39 @@ def test_version_and_errors():
     assert L.vame_cus_per_ctu(0) == 201 and L.vame_cus_per_ctu(1) == 284
 
 
-@pytest.mark.parametrize("tasks,chain,mix,quad_items", [("16", "1", "1", 20), ("16", "1", "0", 24), ("8", "1", "1", 32),
-                                                      ("8", "0", "0", 44), ("4", "0", "0", 72), ("1", "1", "1", 228),
-                                                      ("16", "0", "1", 32)])
-@pytest.mark.parametrize("half128", [1, 0])
-def test_work_items_cover_every_cu_once(half128, tasks, chain, mix, quad_items, monkeypatch):
+def test_work_items_cover_every_cu_once():
     """The engine's work-item templates (vame_create's build_templates, run on
     the host without a device) partition the CTU's candidate CUs: every FULL
     (201) and HALF (284) output offset is covered by exactly one item's CU
-    slot -- with the 128x64 / 64x128 CUs in 512-thread affine_me_half items
-    (one CU each, the default) or packed two per 1024-thread CTU item, and
-    for every quadrant packing: autonomous items of 16 wave tasks (default),
-    8, 4 or 1; the cooperative groups (FULL 64x64 / 64x32 / 32x64, HALF
-    64x32 + 32x64) chained into one item per quadrant (default) or one item
-    each; a launch of both alignments on items mixing them (default) or on
-    the two alignments' own items.  quad_items: the quadrant items per CTU of
-    a both-alignment launch."""
-    monkeypatch.setenv("VAME_TASKS", tasks)
-    monkeypatch.setenv("VAME_CHAIN", chain)
-    monkeypatch.setenv("VAME_MIX", mix)
+    slot -- the 128x128 CU and each 128x64 / 64x128 CU an item of its own;
+    per quadrant, affine_me_quad's items (the 64x64 CU cooperative, the
+    16-sub-block CUs in autonomous items of 16 wave tasks) and
+    affine_me_quad2's (the CUs of 32 to 128 sub-blocks, two stacked
+    sub-blocks per lane, in autonomous items), mixing the alignments in a
+    launch of both (8 + 8 quadrant items per CTU); the PROF packing (every
+    quadrant CU in affine_me_quad) covers alike.  The CTU-item packing of
+    rounds 1-5 is gone (half128 = 0 is rejected)."""
     L = _lib.lib()
     items = (ctypes.c_int32 * 3)()
     for align, n in ((0, 201), (1, 284)):
         hits = (ctypes.c_int32 * n)()
-        assert L.vame_template_coverage(half128, align, hits, items) == 0
+        assert L.vame_template_coverage(1, align, hits, items) == 0
         assert list(hits) == [1] * n, (align, [i for i in range(n) if hits[i] != 1])
+        assert L.vame_template_coverage(0, align, hits, items) == -1
     quad, ctu, half = list(items)
-    assert quad > 0 and quad == (quad_items or quad)
-    assert (ctu, half) == ((1, 4) if half128 else (3, 0))
+    assert (quad, ctu, half) == (16, 1, 4)
+
+
+def test_engine_reads_at_most_five_knobs():
+    """the product library reads at most five environment
+    variables, each documented in include/vame.h."""
+    src = open(os.path.join(os.path.dirname(__file__), "..", "vvc-affine-gpu_amd", "csrc",
+                            "vame_engine.hip")).read()
+    knobs = set(re.findall(r'env_int\("(VAME_[A-Z_]+)"', src))
+    assert src.count("getenv") <= 5 and 0 < len(knobs) <= 5, knobs
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "vame.h")).read()
+    for k in knobs:
+        assert k in hdr, k
 
 
 @pytest.mark.parametrize("row", GOLD["lambda"], ids=lambda r: f"qp{r['qp']}_poc{r['poc']}")
@@ -182,15 +187,19 @@ def test_product_kernels_have_no_scratch():
     -disable-machine-licm and on the kernels' opaque() recomputation, so a
     compiler update or a kernel edit that brings spills back fails here: every
     affine_me_* kernel of the built libvame.so has a zero private segment,
-    except affine_me_half2w / _half2h, whose upper sub-block's prediction stays
-    in registers across the lower one's (16-20 B per lane; parked
-    in LDS instead they ran 8 % slower, three workgroups per CU instead of
-    four), and the PROF variants (not the benchmarked path)."""
+    except the two-sub-block kernels whose upper sub-block's prediction stays
+    in registers across the lower one's: affine_me_half2w / _half2h (16-20 B
+    per lane; parked in LDS instead they ran 8 % slower, three
+    workgroups per CU instead of four) and affine_me_quad2 (24-40 B per lane;
+    parked in LDS: c4 +5 %, c2 +3 %) -- and the PROF variants
+    (not the benchmarked path)."""
     sizes = kernel_scratch(_lib.LIB_PATH)
     product = {k: v for k, v in sizes.items() if "affine_me" in k and "prof" not in k}
-    assert len(product) == 18, sorted(product)
+    assert len(product) == 15, sorted(product)
     for k, v in product.items():
         if "half2" in k:
             assert v <= 24, (k, v)
+        elif "quad2" in k:
+            assert v <= 40, (k, v)
         else:
             assert v == 0, (k, v)

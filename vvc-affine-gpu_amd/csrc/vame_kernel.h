@@ -121,35 +121,13 @@ struct KParams {
 // VAME_DUP (timing-only builds, results stay correct): run a phase twice to
 // price it in throughput terms: bit 0 prediction, bit 1 gradient, bit 2
 // equation reduction, bit 6 the tile staging round trip, bit 4 the solve (on the system itself, before the real
-// one rebuilds it: no extra LDS); with bit 5 set, only in the 3-CP pass.
+// one rebuilds it: no extra LDS); with bit 5 set, only in the 3-CP pass.  The
+// rest of an iteration: bit 7 the CU's MV field (mv_field), bit 8 the extended
+// prediction rows (DPP neighbour columns, edge-row publication and reads),
+// bit 9 the SATD segment sum, bit 10 the cost / best step, bit 11 the CPMV
+// update (scaleDeltaMvs, clamp, clip, rate bits, flag sums).
 #ifndef VAME_DUP
 #define VAME_DUP 0
-#endif
-// SBL = 2: the original rows kept in registers from the prediction to the
-// gradient step instead of read again (VAME_OG_KEEP).
-#ifndef VAME_OG_KEEP
-#define VAME_OG_KEEP 0
-#endif
-// Non-temporal loads for the reference tile's staging (VAME_NT_TILE).
-#ifndef VAME_NT_TILE
-#define VAME_NT_TILE 0
-#endif
-// Wide, batched loads for windows outside the staged tile (filter_rows_global).
-#ifndef VAME_WIDE_GLOBAL
-#define VAME_WIDE_GLOBAL 1
-#endif
-#ifndef VAME_GLOBAL_BATCH
-#define VAME_GLOBAL_BATCH 5
-#endif
-// One filter pass for a whole wave whose windows partly leave the tile.
-#ifndef VAME_MIXED_FILTER
-#define VAME_MIXED_FILTER 1
-#endif
-#ifndef VAME_MIXED_PIPE
-#define VAME_MIXED_PIPE 0
-#endif
-#ifndef VAME_WIDE_X4
-#define VAME_WIDE_X4 1
 #endif
 // Wave priority (s_setprio) during the latency-bound solve: its dependent
 // FP64 / LDS chain issues ahead of other waves' prediction work (~0.5 %;
@@ -203,12 +181,12 @@ __device__ unsigned long long g_pred_count[20];
 #endif
 enum { kPhStage, kPhPredict, kPhCost, kPhGradient, kPhSolve, kPhTail, kPhReduce, kNumPhases };
 #if VAME_PHASE_TIMING
-// [kernel: quad, ctu, half, ctu2, half2w, half2h][phase + kNumPhases for the
+// [kernel: quad, ctu, half, ctu2, half2w, half2h, quad2][phase + kNumPhases for the
 // 3-CP pass; then SIMD-slot use (2), workgroups, workgroup lifetimes]
 // (kPhGradient: the gradient sums; kPhReduce: the equations' reduction and
 // the barrier after it)
 constexpr int kPhSlots = 2 * kNumPhases + 4;
-__device__ unsigned long long g_phase_cycles[6][kPhSlots];
+__device__ unsigned long long g_phase_cycles[7][kPhSlots];
 #define PH_DECL unsigned long long ph_acc[2 * kNumPhases] = {}; unsigned long long ph_t = __builtin_amdgcn_s_memtime(); const unsigned long long ph_t0 = ph_t;
 #define PH_MARK(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_acc[(i) + ph_off] += t_ - ph_t; ph_t = t_; }
 // plus SIMD-slot use: [12] = waves x block lifetime, [13] = sum of wave lifetimes
@@ -521,17 +499,12 @@ __device__ __forceinline__ void frame_row(const uint16_t* __restrict__ ref, int 
     const unsigned a = (unsigned)wx * 2u, b = a & ~3u, sh = (a & 2u) << 3;  // sh: 0 or 16 bits
     const unsigned off = (unsigned)y * (unsigned)W * 2u + b;
     unsigned raw[6];
-#if VAME_WIDE_X4
     // dword-aligned 16 + 8 byte loads (global_load_dwordx4 / x2 need only dword alignment)
     typedef unsigned u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
     typedef unsigned u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
     const u32x4a4 v4 = *reinterpret_cast<const u32x4a4*>(base + off);
     const u32x2a4 v2 = *reinterpret_cast<const u32x2a4*>(base + (off + 16u));
     raw[0] = v4.x; raw[1] = v4.y; raw[2] = v4.z; raw[3] = v4.w; raw[4] = v2.x; raw[5] = v2.y;
-#else
-#pragma unroll
-    for (int k = 0; k < 6; k++) raw[k] = *reinterpret_cast<const unsigned*>(base + (off + 4u * k));
-#endif
 #pragma unroll
     for (int q = 0; q < 5; q++) D[q] = __builtin_amdgcn_alignbit(raw[q + 1], raw[q], sh);
   } else {
@@ -554,13 +527,6 @@ __device__ __forceinline__ void filter_rows_mixed(const unsigned* src, bool inTi
                                                   int H, const uint4& KA, const uint4& KB, const uint4& G0,
                                                   const uint4& G1, int (&acc)[4][4]) {
   const bool wide = wx >= 0 && wx + 12 <= W;
-#if VAME_MIXED_PIPE
-  unsigned Nx[2][5];  // the next row pair from the frame, loaded one step ahead
-  if (!inTile) {
-    frame_row(ref, wx, clampi(wy, 0, H - 1), W, wide, Nx[0]);
-    frame_row(ref, wx, clampi(wy + 1, 0, H - 1), W, wide, Nx[1]);
-  }
-#endif
 #pragma unroll
   for (int k = 0; k < 5; k++) {
     unsigned E[2][5];
@@ -572,22 +538,10 @@ __device__ __forceinline__ void filter_rows_mixed(const unsigned* src, bool inTi
 #pragma unroll
           for (int q = 0; q < 5; q++) E[h][q] = src[row * PITCH_DW + q];
         } else {
-#if VAME_MIXED_PIPE
-#pragma unroll
-          for (int q = 0; q < 5; q++) E[h][q] = Nx[h][q];
-#else
           frame_row(ref, wx, clampi(wy + row, 0, H - 1), W, wide, E[h]);
-#endif
         }
       }
     }
-#if VAME_MIXED_PIPE
-    if (!inTile && k < 4) {
-#pragma unroll
-      for (int h = 0; h < 2; h++)
-        if (2 * k + 2 + h < 9) frame_row(ref, wx, clampi(wy + 2 * k + 2 + h, 0, H - 1), W, wide, Nx[h]);
-    }
-#endif
     int t0[4], t1[4] = {0, 0, 0, 0};
     hrow_raw(E[0], KA, KB, t0);
     if (k < 4) hrow_raw(E[1], KA, KB, t1);
@@ -623,10 +577,10 @@ __device__ __forceinline__ void filter_rows_global(const uint16_t* __restrict__ 
                                                    int W, int H, const uint4& KA, const uint4& KB,
                                                    const unsigned* s_coef_dw, int fy,
                                                    int (&acc)[4][4]) {
-  if (VAME_WIDE_GLOBAL && wx >= 0 && wx + 12 <= W) {
+  if (wx >= 0 && wx + 12 <= W) {
     const char* base = reinterpret_cast<const char*>(ref);
     const unsigned a = (unsigned)wx * 2u, b = a & ~3u, sh = (a & 2u) << 3;  // sh: 0 or 16 bits
-    constexpr int NB = VAME_GLOBAL_BATCH;  // rows whose loads are in flight together
+    constexpr int NB = 5;  // rows whose loads are in flight together
 #pragma unroll 1
     for (int i0 = 0; i0 < 9; i0 += NB) {
       unsigned raw[NB][6];
@@ -849,7 +803,7 @@ __device__ __forceinline__ int predict_sb(const MvField& f, int sx, int sy, cons
   const uint4 KA = s_coef[fx * 3 + sp], KB = s_coef[fx * 3 + sp + 1];
   const uint4 G0 = s_coef[fy * 3 + 0], G1 = s_coef[fy * 3 + 1];
   int acc[4][4];
-  if (VAME_MIXED_FILTER && !PROF) {
+  if (!PROF) {
     // offsets folded into the rows (hrow_raw); the first tap pair overwrites acc (vpair)
 #pragma unroll
     for (int r = 0; r < 4; r++)
@@ -1185,16 +1139,27 @@ struct CuState {
 // 4 / 5 affine_me_half2w / affine_me_half2h -- ONE 128x64 / 64x128 CU per
 // 256-thread workgroup, two stacked sub-blocks per lane, its tile staged over
 // the CU's extent (160 x 96 / 96 x 160, sized for it), four workgroups per CU.
-enum { kKindQuad = 0, kKindCtu = 1, kKindHalf = 2, kKindCtu2 = 3, kKindHalf2W = 4, kKindHalf2H = 5 };
+// 6 affine_me_quad2 -- a 64x64 quadrant's CUs of 32 to 128 sub-blocks, 256
+// threads, two stacked sub-blocks per lane, autonomous wave tasks only (a CU
+// of 32 / 64 / 128 sub-blocks on 16 / 32 / 64 lanes, four / two / one per
+// wave): every per-wave step of an iteration (MV field, cost, equation
+// reduction, solve, update) covers twice the sub-blocks it does in
+// affine_me_quad, which keeps the 16-sub-block CUs and the 64x64 CUs.
+enum { kKindQuad = 0, kKindCtu = 1, kKindHalf = 2, kKindCtu2 = 3, kKindHalf2W = 4, kKindHalf2H = 5, kKindQuad2 = 6 };
+#ifndef VAME_QUAD2_STASH
+#define VAME_QUAD2_STASH 0
+#endif
 template <int KIND>
 struct Cfg {
   static constexpr bool HALF2 = KIND == kKindHalf2W || KIND == kKindHalf2H;
-  static constexpr int REGION = KIND == kKindQuad ? 64 : 128;  // largest region edge
-  static constexpr int THREADS = KIND == kKindQuad || HALF2 ? 256 : KIND == kKindCtu ? 1024 : 512;
-  static constexpr int SBL = KIND == kKindCtu2 || HALF2 ? 2 : 1;  // sub-blocks per lane (stacked vertically)
+  static constexpr bool QUAD = KIND == kKindQuad || KIND == kKindQuad2;  // quadrant work items
+  static constexpr int REGION = QUAD ? 64 : 128;  // largest region edge
+  static constexpr int THREADS = QUAD || HALF2 ? 256 : KIND == kKindCtu ? 1024 : 512;
+  static constexpr int SBL = KIND == kKindCtu2 || HALF2 || KIND == kKindQuad2 ? 2 : 1;  // sub-blocks per lane (stacked vertically)
   static constexpr int MAXCU = (KIND == kKindHalf || KIND == kKindCtu2 || HALF2) ? 1 : kMaxCu;  // CU state slots (LDS)
-  static constexpr int ITEMCU = KIND == kKindQuad ? kItemCu : MAXCU;  // CU slots per item
-  static constexpr bool AUTO = KIND == kKindQuad;       // holds autonomous items
+  static constexpr int ITEMCU = QUAD ? kItemCu : MAXCU;  // CU slots per item
+  static constexpr bool AUTO = QUAD;                    // holds autonomous items
+  static constexpr bool COOP = KIND != kKindQuad2;      // holds cooperative items
   static constexpr int MARGIN = 16;                     // reference-tile margin (samples)
   static constexpr int TILE = REGION + 2 * MARGIN;      // tile edge (samples; the staged extent's largest)
   static constexpr int TILE_W = KIND == kKindHalf2H ? 64 + 2 * MARGIN : TILE;  // allocated tile extent
@@ -1204,17 +1169,12 @@ struct Cfg {
   static constexpr int TP = (TILE_W + 7) / 16 * 16 + 8;
   static constexpr int TILE_ELEMS = TILE_H * TP + 16;
   static constexpr int NSB = THREADS * SBL;             // sub-blocks per work item (max)
-#ifndef VAME_STASH
-#define VAME_STASH 1
-#endif
   // SBL = 2: the upper sub-block's prediction parked in LDS across the lower
-  // one's (VAME_STASH=0: held in registers)
-  // (affine_me_half2*: in registers, so that four workgroups fit a CU's LDS;
-  // VAME_HALF2_STASH=1 parks it there too, three workgroups per CU)
-#ifndef VAME_HALF2_STASH
-#define VAME_HALF2_STASH 0
-#endif
-  static constexpr bool STASH = VAME_STASH != 0 && (!HALF2 || VAME_HALF2_STASH != 0);
+  // one's (held in registers: +3 % time at c4); affine_me_half2* keep it in
+  // registers, so that four workgroups fit a CU's LDS (parked in LDS, three
+  // per CU: 8 % slower, HISTORY.md)
+  // (affine_me_quad2: in registers, VAME_QUAD2_STASH=1 parks it in LDS)
+  static constexpr bool STASH = KIND == kKindQuad2 ? VAME_QUAD2_STASH != 0 : !HALF2;
 };
 
 // Value i of a sub-block's contribution to its CU's normal equations
@@ -1635,15 +1595,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         const int fy = clampi(ty0 + ty, 0, H - 1), fx = tx0 + cx;
         const uint16_t* row = ref + (size_t)fy * W;
         if (fx >= 0 && fx + 7 < W) {
-#if VAME_NT_TILE
-          // read once per item: a non-temporal load, so the reference rows do
-          // not push the CU's original samples (re-read every iteration) out of L2
-          typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-          const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + fx));
-          tv[j] = make_uint4(v.x, v.y, v.z, v.w);
-#else
           tv[j] = *reinterpret_cast<const uint4*>(row + fx);
-#endif
         } else {
           unsigned a[8];
 #pragma unroll
@@ -1674,7 +1626,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   PH_START
   const int hdr = __builtin_amdgcn_readfirstlane(s_hdr[0]);
   const int nTasks = (hdr >> 16) & 0xFF;
-  const bool coop = !C::AUTO || (hdr & 1) != 0;
+  const bool coop = C::COOP && (!C::AUTO || (hdr & 1) != 0);
   const bool claim = C::AUTO && (hdr & 2) != 0;  // autonomous: waves claim tasks as they finish
   PH_MARK(kPhStage)
   if (!coop && wv >= nTasks) {  // wave-uniform: an autonomous wave without CUs
@@ -1840,6 +1792,19 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           int cp[6];
           for (int i = 0; i < 6; i++) cp[i] = s_st[myCu].cur[i];
           const MvField f = mv_field(cp, ncp, gp.lw, gp.lh);
+          if constexpr ((kDup & 128) != 0) {  // timing-only: the MV field again
+            int cp2[6];
+            for (int i = 0; i < 6; i++) cp2[i] = cp[i];
+            int lw2 = gp.lw;
+            opaque(cp2[0]);
+            opaque(lw2);
+            const MvField f2 = mv_field(cp2, ncp, lw2, gp.lh);
+            if (ncp == 3)
+              asm volatile("" ::"v"(f2.bx), "v"(f2.by), "v"(f2.hx), "v"(f2.hy), "v"(f2.vx), "v"(f2.vy),
+                           "v"((int)f2.spread));
+            else
+              asm volatile("" ::"v"(f2.bx), "v"(f2.by), "v"(f2.hx), "v"(f2.hy), "v"((int)f2.spread));
+          }
           int satdLane = 0;
 #pragma unroll
           for (int j = 0; j < SBL; j++) {
@@ -1881,6 +1846,25 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
           }
           s_top[sbIdx] = Pr[0][0];
           s_bot[sbIdx] = Pr[SBL - 1][3];
+          if constexpr ((kDup & 256) != 0) {  // timing-only: the extended rows and edge stores again
+            int i2 = sbIdx;
+            opaque(i2);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              uint2 q = Pr[0][r];
+              opaque(reinterpret_cast<int&>(q.x));
+              const uint4 x2 = ext_row(q, dpp32<0x138, 0xF>((int)q.y), dpp32<0x130, 0xF>((int)q.x));
+              asm volatile("" ::"v"(x2.x), "v"(x2.w));
+            }
+            s_top[i2] = Pr[0][0];
+            s_bot[i2] = Pr[SBL - 1][3];
+          }
+          if constexpr ((kDup & 512) != 0) {  // timing-only: the SATD segment sum again
+            int s2 = satdLane;
+            opaque(s2);
+            const int v2 = logS == 4 ? seg_sum_c<4>(s2) : logS == 5 ? seg_sum_c<5>(s2) : seg_sum_c<6>(s2);
+            asm volatile("" ::"v"(v2));
+          }
           const int v = logS == 4 ? seg_sum_c<4>(satdLane)
                         : logS == 5 ? seg_sum_c<5>(satdLane) : seg_sum_c<6>(satdLane);
           if (leader) {
@@ -1899,6 +1883,21 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
         // 2189) kept in CuState by the update step; the strict best is kept.
         const bool lastIter = iter == niter;
         bool better = false;  // keepS: this lane's CU improved
+        if constexpr ((kDup & 1024) != 0) {  // timing-only: the pricing again (before the real one)
+          int bet2 = 0;
+          if (myCu >= 0 && (keepS || local == 7)) {
+            const CuState& st = s_st[myCu];
+            int r2 = st.rate;
+            opaque(r2);
+            if (iter == 0 || st.live) {
+              const float prod = __fmul_rn(pa.lambda, (float)(r2 + kRuiBits));
+              const long long cost = (long long)st.satd + (long long)(int)floorf(prod);
+              bet2 = cost < st.bestCost;
+            }
+          }
+          if (!keepS) bet2 = __builtin_amdgcn_update_dpp(0, bet2, 0x157, 0xF, 0xF, false);
+          asm volatile("" ::"v"(bet2));
+        }
         if constexpr (!keepS) {
           // the CU's lane 7 prices and keeps the best; lanes 0-5 copy the CPMVs
           int bet = 0;
@@ -1974,6 +1973,14 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             if constexpr (SBL == 2) opaque(nbIdx);  // recomputed, not hoisted (VGPRs)
             const uint2 tb = s_bot[max(nbIdx - sbCols, 0)], bt = s_top[min(nbIdx + sbCols, C::THREADS - 1)];
             X[0] = ext_row(tb, dpp32<0x138, 0xF>((int)tb.y), dpp32<0x130, 0xF>((int)tb.x));
+            if constexpr ((kDup & 256) != 0) {  // timing-only: the neighbours' edge rows again
+              int n2 = nbIdx;
+              opaque(n2);
+              const uint2 tb2 = s_bot[max(n2 - sbCols, 0)], bt2 = s_top[min(n2 + sbCols, C::THREADS - 1)];
+              const uint4 a2 = ext_row(tb2, dpp32<0x138, 0xF>((int)tb2.y), dpp32<0x130, 0xF>((int)tb2.x));
+              const uint4 b2 = ext_row(bt2, dpp32<0x138, 0xF>((int)bt2.y), dpp32<0x130, 0xF>((int)bt2.x));
+              asm volatile("" ::"v"(a2.x), "v"(a2.w), "v"(b2.x), "v"(b2.w));
+            }
             Geo gg = g;
             int sxg = sx, syg = sy;
             if constexpr (SBL == 2) opaque_geo(gg, sxg, syg);
@@ -1996,7 +2003,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
                                      dpp32<0x130, 0xF>((int)Pr[j][r].x));
                 const uint2 nb = j + 1 < SBL ? Pr[j + 1][0] : bt;
                 X[5] = ext_row(nb, dpp32<0x138, 0xF>((int)nb.y), dpp32<0x130, 0xF>((int)nb.x));
-                if (!VAME_OG_KEEP) {
+                {
                   const unsigned b0 = (unsigned)((gg.y + syg + 4 * j) * W + gg.x + sxg) * 2u, bw = (unsigned)W * 2u;
                   const char* base = reinterpret_cast<const char*>(cur);
 #pragma unroll
@@ -2088,6 +2095,30 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
             st.satd = 0;
           }
           bool liveNew = false;
+          if constexpr ((kDup & 2048) != 0) {  // timing-only: the update again, without its stores
+            if (act && loc < 8) {
+              const CuState& st = s_st[cuS];
+              int f = 0, q = 0;
+              if (loc < 2 * ncp) {
+                int j = loc;
+                opaque(j);
+                const double d = M[j == 1 ? 2 : j == 2 ? 1 : j];
+                const int cj = st.cur[j], pj = st.prev[j];
+                int v = (int)((unsigned)cj + (unsigned)scale_delta(d));
+                v = clampi(v, kMvMin, kMvMax);
+                const int pos = (j & 1) ? ctuY + cs.y : ctuX + cs.x, lim = (j & 1) ? H : W;
+                v = clampi(v, shl(-128 - 8 - pos + 1, 4), shl(lim + 8 - pos - 1, 4));
+                f = (v != cj ? 1 : 0) | (v != pj ? 16 : 0);
+                q = to_quarter(v);
+              }
+              const int q2 = dpp32<0x112, 0xF>(q), q4 = dpp32<0x114, 0xF>(q);
+              if (loc < 2 * ncp) f += eg_bits(q - (loc >= 4 ? q4 : loc >= 2 ? q2 : 0)) << 8;
+              f += dpp32<0x111, 0xF>(f);
+              f += dpp32<0x112, 0xF>(f);
+              f += dpp32<0x114, 0xF>(f);
+              asm volatile("" ::"v"(f));
+            }
+          }
           if (act && loc < 8) {
             CuState& st = s_st[cuS];
             int f = 0, q = 0;
@@ -2162,14 +2193,16 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
     using F = std::false_type;
     // keepS: the 2-CP pass feeds a 3-CP pass (seed reuse)
     using KeepS = std::integral_constant<bool, run3>;
-    if (coop) {
-      if constexpr (run2) run_pass(I2{}, T{}, KeepS{});
-      if constexpr (run3) run_pass(I3{}, T{}, F{});
+    if (C::COOP && coop) {
+      if constexpr (C::COOP) {
+        if constexpr (run2) run_pass(I2{}, T{}, KeepS{});
+        if constexpr (run3) run_pass(I3{}, T{}, F{});
+      }
     } else {
       if constexpr (run2) run_pass(I2{}, F{}, KeepS{});
       if constexpr (run3) run_pass(I3{}, F{}, F{});
     }
-    if (KIND != kKindQuad) break;  // 128-class items: one task
+    if (!C::QUAD) break;  // 128-class items: one task
     // the next task's CU slots into this task's (cooperative: after every wave's
     // last read of them, autonomous: the wave's own, read by this wave only)
     int next = task + (coop ? 1 : 4);
@@ -2200,15 +2233,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     KParams p) {
   affine_me_body<kKindQuad, false, MODE>(p);
 }
-// 128-class items: one 1024-thread workgroup per CU (~100 KB of LDS), one lane
-// per sub-block of a 128x128 CU.
+// The quadrant CUs of 32 to 128 sub-blocks, two stacked sub-blocks per lane
+// (autonomous wave tasks only): 4 workgroups per CU, 128 VGPRs.
 template <int MODE>
-__global__ __launch_bounds__(1024) void affine_me_ctu(KParams p) { affine_me_body<kKindCtu, false, MODE>(p); }
-// One 128x64 / 64x128 CU per 512-thread workgroup, two per CU (~74 KB of LDS
-// each): 128 VGPRs so both fit.
-template <int MODE>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_half(KParams p) {
-  affine_me_body<kKindHalf, false, MODE>(p);
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad2(
+    KParams p) {
+  affine_me_body<kKindQuad2, false, MODE>(p);
 }
 // ONE 128x128 CU per 512-thread workgroup, two stacked sub-blocks per lane,
 // two workgroups per CU (~72 KB of LDS each; the 3-CP seed-reuse sums in
@@ -2227,7 +2257,10 @@ template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_half2h(KParams p) {
   affine_me_body<kKindHalf2H, false, MODE>(p);
 }
-// The same with PROF (vame_set_prof).
+// The same with PROF (vame_set_prof): the quadrant items; the 128x128 CU in
+// one 1024-thread workgroup per CU (~100 KB of LDS), one lane per sub-block;
+// each 128x64 / 64x128 CU in a 512-thread workgroup, two per CU (~74 KB of
+// LDS each).
 template <int MODE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad_prof(
     KParams p) {

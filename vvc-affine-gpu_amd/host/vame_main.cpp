@@ -31,10 +31,12 @@
 //    reference's per-PRED *_EXEC keys carry the fused kernel time apportioned
 //    by each PRED's algorithmic work (sub-block predictions of its in-frame
 //    CUs, n_pred = 6 for 2 CP / 5 for 3 CP, + ExtraGradientIter); they sum to
-//    FUSED_POC_EXEC, the measured time.  --per-launch measures them directly;
-//  * extra keys after the reference's: READ_CSV_TIME (ingest), LOG_WRITE_TIME
-//    (host time formatting + writing the logs, overlapped with the GPU),
-//    LOG_BYTES.
+//    FUSED_POC_EXEC, the measured time, and PRED_EXEC_SOURCE says so
+//    ("estimated-apportioned"; "measured" with --per-launch, which times each
+//    launch as the reference does);
+//  * extra keys after the reference's: FUSED_POC_EXEC, PRED_EXEC_SOURCE,
+//    READ_CSV_TIME (ingest), LOG_WRITE_TIME (host time formatting + writing
+//    the logs, overlapped with the GPU), LOG_BYTES.
 #include <hip/hip_runtime.h>
 #include <sys/time.h>
 #include <time.h>
@@ -355,6 +357,9 @@ void gpu_worker(Job J) {
   GPU_CHECK(hipSetDevice(J.device), "hipSetDevice");
   vame_ctx* ctx = nullptr;
   VAME_CHECK(vame_create(&ctx, J.device, J.W, J.H), "vame_create");
+  // a batch holds at most kBatchPocs POCs of <= 4 pairs: the seed-reuse
+  // scratch for that many pairs per launch (half of the default)
+  VAME_CHECK(vame_set_max_pairs(ctx, 4 * kBatchPocs), "vame_set_max_pairs");
   const double w1 = now_s();
   VAME_CHECK(vame_set_prof(ctx, J.prof ? 1 : 0), "vame_set_prof");
   hipStream_t st, up, dn;  // compute; frame uploads; result downloads
@@ -944,6 +949,10 @@ int main(int argc, char** argv) {
   printf("TOTAL_EXEC_TIME(%dx),%f\n", N, total_ns);
   printf("OVERALL(%dx),%f\n", N, (double)(float)overall);
   if (!per_launch) printf("FUSED_POC_EXEC,%f\n", (double)fused_ns);
+  // how the four per-PRED keys above were obtained: measured per launch
+  // (--per-launch, the reference's events), or -- one fused launch computes
+  // all four PREDs -- the measured fused time apportioned by algorithmic work
+  printf("PRED_EXEC_SOURCE,%s\n", per_launch ? "measured" : "estimated-apportioned");
   printf("READ_CSV_TIME,%f\n", read_s * 1e9);
   printf("LOG_WRITE_TIME,%f\n", log_s * 1e9);
   printf("LOG_BYTES,%lld\n", log_bytes);

@@ -19,7 +19,7 @@ EXPORTS = (
     "vame_log_writer_refs", "vame_read_frames_range", "vame_count_lines", "vame_read_frames_span",
     "vame_log_writer_set_deferred", "vame_log_writer_num_files", "vame_log_writer_file_name",
     "vame_log_writer_sizes", "vame_log_writer_flush_at", "vame_template_coverage", "vame_pack_records",
-    "vame_count_lines_ranges",
+    "vame_count_lines_ranges", "vame_set_max_pairs", "vame_get_max_pairs",
 )
 
 
@@ -68,6 +68,8 @@ def lib():
         L.vame_version.restype = ctypes.c_char_p
         L.vame_set_timing.argtypes = [P, I]
         L.vame_set_prof.argtypes = [P, I]
+        L.vame_set_max_pairs.argtypes = [P, I]
+        L.vame_get_max_pairs.argtypes = [P]
         L.vame_get_timing.argtypes = [P, I, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_int), I]
         C = ctypes.c_char_p

@@ -65,6 +65,15 @@ class Engine:
         affine.cl:168); vame_set_prof."""
         check(lib().vame_set_prof(self._h, int(enable)))
 
+    def set_max_pairs(self, n: int) -> None:
+        """(POC, refIdx) pairs per launch, 1..32 (default 32): sizes the
+        context's 3-CP seed-reuse scratch (vame_set_max_pairs)."""
+        check(lib().vame_set_max_pairs(self._h, int(n)))
+
+    @property
+    def max_pairs(self) -> int:
+        return lib().vame_get_max_pairs(self._h)
+
     def set_timing(self, enable, keep: bool = False) -> None:
         """True / 1: time every kernel class; 2: the quadrant kernel only; 0: off.
         keep: leave the launches recorded so far (VAME_TIMING_KEEP)."""
@@ -72,9 +81,9 @@ class Engine:
 
     def get_timing(self, kernel_class: int, reset: bool = True):
         """(total_ms, launches) of kernel class 0 (quadrant items, affine_me_quad) /
-        1 (CTU items, affine_me_ctu) / 2 (128x64 and 64x128 CUs, affine_me_half) /
         3 (128x128 CUs, affine_me_ctu2) / 4, 5 (128x64 / 64x128 CUs,
-        affine_me_half2w / affine_me_half2h)."""
+        affine_me_half2w / affine_me_half2h); under PROF 1 (128x128 CUs,
+        affine_me_ctu_prof) / 2 (128x64 and 64x128 CUs, affine_me_half_prof)."""
         t, n = ctypes.c_double(), ctypes.c_int()
         check(lib().vame_get_timing(self._h, kernel_class, ctypes.byref(t), ctypes.byref(n), int(reset)))
         return t.value, n.value
@@ -144,7 +153,8 @@ class Engine:
 
     def affine_me_batch(self, jobs, modes: int = 3, extra: int = 0):
         """jobs: [(cur, refs, lam, out)] with out from alloc_poc; one
-        vame_affine_me_batch call (32 (POC, refIdx) pairs per launch)."""
+        vame_affine_me_batch call (max_pairs (POC, refIdx) pairs per launch,
+        default 32)."""
         keep = []
         arr = (PocJob * len(jobs))()
         for j, (cur, refs, lam, out) in enumerate(jobs):

@@ -34,11 +34,13 @@ def cu_inventory(W: int, H: int):
 
 def pair_accounting(W: int, H: int, ncps=(2,), extra: int = 0):
     """Per (POC, ref) pair: rows, in-frame rows, and B_alg split by kernel class
-    ('quad' = affine_me_quad items, 'big' = the 128-class CUs: 'ctu' = the
-    128x128 CUs of affine_me_ctu, 'half' = the 128x64 / 64x128 CUs of
-    affine_me_half)."""
-    acc = {"rows": 0, "rows_inframe": 0, "bytes_quad": 0, "bytes_big": 0, "bytes_ctu": 0,
-           "bytes_half": 0, "bytes_half_w": 0, "bytes_half_h": 0, "sb_pred": 0, "sb_pred_quad": 0,
+    ('quad' = the quadrant CUs: 'quad1' = those of affine_me_quad -- 16
+    sub-blocks, and the 64x64 CUs -- and 'quad2' = those of affine_me_quad2 --
+    32 to 128 sub-blocks; 'big' = the 128-class CUs: 'ctu' = the 128x128 CUs of
+    affine_me_ctu2, 'half' = the 128x64 / 64x128 CUs of affine_me_half2w /
+    _half2h)."""
+    acc = {"rows": 0, "rows_inframe": 0, "bytes_quad": 0, "bytes_quad1": 0, "bytes_quad2": 0, "bytes_big": 0,
+           "bytes_ctu": 0, "bytes_half": 0, "bytes_half_w": 0, "bytes_half_h": 0, "sb_pred": 0, "sb_pred_quad": 0,
            "sb_pred_big": 0}
     inv = cu_inventory(W, H)
     for ncp in ncps:
@@ -53,6 +55,8 @@ def pair_accounting(W: int, H: int, ncps=(2,), extra: int = 0):
                 acc["sb_pred"] += npred * nsb
                 acc["sb_pred_big" if big else "sb_pred_quad"] += npred * nsb
             acc["bytes_big" if big else "bytes_quad"] += b
+            if not big:
+                acc["bytes_quad2" if 32 <= (w // 4) * (h // 4) <= 128 else "bytes_quad1"] += b
             if big:
                 acc["bytes_ctu" if w == h else "bytes_half"] += b
                 if w != h:  # 128x64 (affine_me_half2w) / 64x128 (affine_me_half2h)
