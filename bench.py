@@ -35,7 +35,7 @@ gathered records byte for byte.  Every line (N = 1 too) then carries
 (--fs-frames, default 48 POCs = 186 pairs) over the N ranks with the gather
 into rank 0 inside its timed span.  Rank 0 prints one JSON line.
 
-`roofline`: the dominant kernel (affine_me_quad) is VALU-issue
+`roofline`: the dominant kernel (affine_me_quad2) is VALU-issue
 bound; `frac` = SQ_INSTS_VALU per launch (committed rocprofv3 profile of the
 config, profiles/pmc_<config>.json) over the live launch time and the wave64
 issue ceiling.  The HBM views ride beside it: measured traffic, the
@@ -179,10 +179,11 @@ def main():
     for _ in range(args.warmup):
         run.step()
     barrier()
-    # HIP events on the dominant (quadrant) kernel's dispatches of the timed
-    # steps; the 128-class kernels are timed on extra steps after them (timing
-    # their dispatches too cost ~0.7 % of a c2 step).  Diagnostic override
-    # VAME_BENCH_KTIMING: 0 = no events, 1 = every kernel in the timed steps.
+    # HIP events on the quadrant kernels' dispatches of the timed steps
+    # (affine_me_quad2, the dominant one, and affine_me_quad); the 128-class
+    # kernels are timed on extra steps after them (timing their dispatches too
+    # cost ~0.7 % of a c2 step).  Diagnostic override VAME_BENCH_KTIMING: 0 = no
+    # events, 1 = every kernel in the timed steps.
     ktiming = int(os.environ.get("VAME_BENCH_KTIMING", "2"))
     # the events ride on a sample of the timed steps -- every ksample-th step
     # (VAME_BENCH_KSAMPLE, default 4) -- so the timed span carries a quarter of
@@ -214,12 +215,12 @@ def main():
     step_ms = sorted(a_.elapsed_time(b_) for a_, b_ in step_ev)
     if not step_ms:  # fewer timed steps than one sample period
         step_ms = [elapsed * 1e3 / max(args.steps, 1)]
-    quad_ms, quad_n = eng.get_timing(0)
-    # the 128-class kernels (CTU items: affine_me_ctu, class 1; 128x64 /
-    # 64x128 CUs: affine_me_half, class 2, or affine_me_half2w / _half2h,
-    # classes 4 / 5; 128x128 CUs: affine_me_ctu2, class 3), timed in the
-    # sampled timed steps with VAME_BENCH_KTIMING=1, else on extra untimed
-    # steps after them
+    quad_ms, quad_n = eng.get_timing(0)    # affine_me_quad
+    quad2_ms, quad2_n = eng.get_timing(6)  # affine_me_quad2
+    # the 128-class kernels (128x128 CUs: affine_me_ctu2, class 3; 128x64 /
+    # 64x128 CUs: affine_me_half2w / _half2h, classes 4 / 5; under PROF 1 / 2),
+    # timed in the sampled timed steps with VAME_BENCH_KTIMING=1, else on extra
+    # untimed steps after them
     BIG = (1, 2, 3, 4, 5)
     big_t = {k: eng.get_timing(k) for k in BIG}
     big_on = "the sampled timed steps"
@@ -230,6 +231,7 @@ def main():
             run.step()
         big_t = {k: eng.get_timing(k) for k in BIG}
         eng.get_timing(0)
+        eng.get_timing(6)
         big_on = f"{big_steps} untimed steps after the timed ones"
     eng.set_timing(False)
     span_ms, span_n = (0.0, 0) if args.no_spans else span_step()
@@ -279,14 +281,21 @@ def main():
                            "check": run.verify_own()})
 
     # the kernels' time per launch (sampled HIP events on their own dispatches)
-    launches_per_step = -(-run.pairs // 32)
+    launches_per_step = -(-run.pairs // eng.max_pairs)
     prof = load_profile(args.config)
     pc = prof.get("pred_count") or {}
     # the algorithmic bytes of one launch of each kernel class (per launch:
     # the launches of a step split its pairs; the events' launches are counted)
     per_launch = lambda key: acc[key] * run.pairs / launches_per_step  # noqa: E731
-    quad_avg = quad_ms / quad_n if quad_n else 0.0
-    roof_q = kernel_roof(quad_avg, per_launch("bytes_quad"), prof.get("kernels", {}).get("affine_me_quad"),
+    # the dominant kernel: affine_me_quad2 (the quadrant CUs of 32-128
+    # sub-blocks, two per lane) when the build splits the quadrant CUs,
+    # else affine_me_quad (every quadrant CU); the executed-prediction
+    # fraction is counted over both quadrant kernels together
+    qsplit = quad2_n > 0
+    dom, dom_key = ("affine_me_quad2", "bytes_quad2") if qsplit else ("affine_me_quad", "bytes_quad")
+    dom_ms, dom_n = (quad2_ms, quad2_n) if qsplit else (quad_ms, quad_n)
+    quad_avg = dom_ms / dom_n if dom_n else 0.0
+    roof_q = kernel_roof(quad_avg, per_launch(dom_key), prof.get("kernels", {}).get(dom),
                          pc.get("executed_pred_frac_quad"))
     # per 128-class kernel, the algorithmic bytes it carries: the 128x128 CUs
     # run in affine_me_ctu2 (the default) or in CTU items; the 128x64 / 64x128
@@ -299,8 +308,16 @@ def main():
     mixed = split and (n_half != big_t[1][1] if not ctu2 else big_t[1][1] > 0)
     ctu_key = ("bytes_half" if ctu2 else "bytes_ctu") if split or ctu2 else "bytes_big"
     big_kernels = {}
+    if qsplit and quad_n:  # affine_me_quad beside it: the 16-sub-block and 64x64 CUs
+        big_kernels["affine_me_quad"] = {"timed_on": "the sampled timed steps", "launches": quad_n,
+                                         **kernel_roof(quad_ms / quad_n, per_launch("bytes_quad1"),
+                                                       prof.get("kernels", {}).get("affine_me_quad"),
+                                                       pc.get("executed_pred_frac_quad"))}
+    # class 4 alone: both orientations in one affine_me_half2 launch
+    half2 = big_t[4][1] > 0 and big_t[5][1] == 0
     for k, name, key in ((1, "affine_me_ctu", ctu_key), (2, "affine_me_half", "bytes_half"),
-                         (3, "affine_me_ctu2", "bytes_ctu"), (4, "affine_me_half2w", "bytes_half_w"),
+                         (3, "affine_me_ctu2", "bytes_ctu"),
+                         (4, "affine_me_half2", "bytes_half") if half2 else (4, "affine_me_half2w", "bytes_half_w"),
                          (5, "affine_me_half2h", "bytes_half_h")):
         ms, n = big_t[k]
         if n == 0 or (mixed and k == 1):
@@ -328,11 +345,12 @@ def main():
         # VALU issue -- SQ_INSTS_VALU per launch over this run's launch time,
         # against the wave64 issue ceiling of 1,024 SIMDs at the peak clock
         "bound": "valu",
-        "kernel": "affine_me_quad",
-        # the engine issues the 128-class kernels on the caller's stream and the
-        # quadrant kernel on a side stream (VAME_STREAMS=2): they run
-        # side by side, so this kernel's launch time includes their share of the
-        # GPU; step.valu_frac counts every kernel's instructions over the step
+        "kernel": dom,
+        # the engine issues affine_me_quad2 on a side stream and the 128-class
+        # kernels and affine_me_quad on the caller's stream (VAME_STREAMS=2,
+        # DESIGN §4): they run side by side, so this kernel's launch time
+        # includes their share of the GPU; step.valu_frac counts every kernel's
+        # instructions over the step
         "concurrent_with": sorted(big_kernels) if os.environ.get("VAME_STREAMS", "2") != "1" else [],
         "achieved": roof_q.get("valu_Ginst_per_s"),
         "peak": VALU_PEAK_GINST,
@@ -363,7 +381,7 @@ def main():
         # of a traced run of this config, the committed profile the counter
         # fields come from, the workload it was taken on, whether that is this
         # line's workload and whether it ran the library this line loaded
-        "rocprof_avg_ms": (prof.get("kernels", {}).get("affine_me_quad") or {}).get("timed_avg_ms"),
+        "rocprof_avg_ms": (prof.get("kernels", {}).get(dom) or {}).get("timed_avg_ms"),
         "profile": prof.get("profile"),
         "profiled_workload": prof.get("profiled_workload"),
         "profile_matches_workload": profile_matches(prof, cfg, run, world, args.rank_only),

@@ -37,16 +37,18 @@ constexpr int kTimingClasses = 7;
 
 struct vame_ctx {
   int device, W, H, nCtus, ctusPerRow;
-  // device-resident work-item templates: the quadrant items of three kernel
-  // sets [s][FULL | HALF | both alignments] at dQuad + quadOff[s][a], s = 0
-  // affine_me_quad and 1 affine_me_quad2 (the split packing), 2 the PROF
-  // packing (every quadrant CU in affine_me_quad_prof); and the 128-class CUs,
+  // device-resident work-item templates: the quadrant items of four sets
+  // [s][FULL | HALF | both alignments] at dQuad + quadOff[s][a]: 3 the SBL1
+  // and SBL2 items together (one affine_me_quad launch: the 2-CP-only
+  // launches), 0 / 1 the SBL1 / SBL2 items apart (affine_me_quad beside
+  // affine_me_quad2: the 2+3-CP launches), 2 the PROF packing (every quadrant
+  // CU one sub-block per lane, affine_me_quad_prof); and the 128-class CUs,
   // each a workgroup of its own: the 128x128 CU (dBig1: affine_me_ctu2;
   // affine_me_ctu_prof under PROF) and every 128x64 / 64x128 CU (dHalfW /
   // dHalfH: affine_me_half2w / _half2h; both in dHalf for affine_me_half_prof
   // under PROF)
   Item* dQuad = nullptr;
-  int quadOff[3][3] = {}, quadN[3][3] = {};
+  int quadOff[4][3] = {}, quadN[4][3] = {};
   Item* dBig1 = nullptr;
   Item* dHalf = nullptr;
   Item* dHalfW = nullptr;
@@ -81,7 +83,8 @@ struct vame_ctx {
   // the barrier bit, the others after it in any order.
   int streams = 2;
   hipStream_t side = nullptr;
-  hipEvent_t evFork = nullptr, evJoin = nullptr;
+  hipStream_t side2 = nullptr;  // timing builds VAME_Q1_SIDE=2: affine_me_quad on a stream of its own
+  hipEvent_t evFork = nullptr, evJoin = nullptr, evJoin2 = nullptr;
   // VAME_SYNC (default 1): the join as a stream memory operation -- the side
   // stream writes a sequence number to a signal-memory word
   // (hipStreamWriteValue32, ordered after its earlier work), the caller's
@@ -221,7 +224,7 @@ Item make_auto_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& task
   memset(&it, 0, sizeof(it));
   it.rx = (int16_t)rx;
   it.ry = (int16_t)ry;
-  it.coop = 2;  // bit 1: waves claim tasks
+  it.coop = sbl == 2 ? 2 | 4 : 2;  // bit 1: waves claim tasks; bit 2: two sub-blocks per lane
   if (tasks.empty() || (int)tasks.size() > kMaxTasks) abort();
   it.nTasks = (int16_t)tasks.size();
   it.nCu = (int16_t)(tasks.size() * kTaskCu);
@@ -241,8 +244,11 @@ Item make_auto_item(int rx, int ry, const std::vector<std::vector<CuDesc>>& task
 // CUs of one quadrant: wave tasks of one size class (largest first, at most
 // kTaskCu CUs and 64 lanes each), then items of kMaxTasks consecutive tasks.
 // Returns the number of items appended.
+#ifndef VAME_Q2_TASKS  // timing builds: wave tasks per affine_me_quad2 item
+#define VAME_Q2_TASKS 16
+#endif
 size_t pack_autonomous(int qx, int qy, std::vector<CuDesc> cus, std::vector<Item>& out, int sbl) {
-  constexpr int perItem = kMaxTasks;
+  const int perItem = sbl == 2 ? VAME_Q2_TASKS : kMaxTasks;
   std::stable_sort(cus.begin(), cus.end(),
                    [](const CuDesc& a, const CuDesc& b) { return nsb_of(a) > nsb_of(b); });
   std::vector<std::vector<CuDesc>> waves;
@@ -383,8 +389,8 @@ void build_templates(std::vector<Item>& big, std::vector<Item>& halfItems, QuadS
 // NSB; quad2: sized for its largest item set).
 size_t best_layout(const vame_ctx* c, int pairs, size_t off[4]) {
   const size_t per = (size_t)pairs * c->nCtus * 5;
-  int nq2 = 0;
-  for (int a = 0; a < 3; a++) nq2 = std::max(nq2, c->quadN[1][a]);
+  int nq2 = 0;  // the SBL2 items index the region by their item index
+  for (int a = 0; a < 3; a++) nq2 = std::max({nq2, c->quadN[1][a], c->quadN[3][a]});
   off[0] = 0;
   off[1] = off[0] + per * c->nBig1 * Cfg<kKindCtu2>::NSB;
   off[2] = off[1] + per * c->nHalfW * Cfg<kKindHalf2W>::NSB;
@@ -515,6 +521,8 @@ KernelFn kernel_for(int mode) {
     return mode == 1 ? affine_me_ctu2<1> : mode == 2 ? affine_me_ctu2<2> : affine_me_ctu2<3>;
   } else if constexpr (KIND == kKindQuad2) {
     return mode == 1 ? affine_me_quad2<1> : mode == 2 ? affine_me_quad2<2> : affine_me_quad2<3>;
+  } else if constexpr (KIND == kKindHalf2W + 100) {  // both orientations (affine_me_half2)
+    return mode == 1 ? affine_me_half2<1> : mode == 2 ? affine_me_half2<2> : affine_me_half2<3>;
   } else if constexpr (KIND == kKindCtu) {  // PROF only
     return mode == 1 ? affine_me_ctu_prof<1> : mode == 2 ? affine_me_ctu_prof<2> : affine_me_ctu_prof<3>;
   } else if constexpr (KIND == kKindHalf) {  // PROF only
@@ -541,18 +549,31 @@ hipError_t launch_kernel(K kernel, unsigned grid, unsigned threads, hipStream_t 
   return hipGetLastError();
 }
 
+// the 128x64 and 64x128 CUs in one launch (affine_me_half2), or in
+// affine_me_half2w then affine_me_half2h (VAME_HALF_MERGE=0 timing builds)
+#ifndef VAME_HALF_MERGE
+#define VAME_HALF_MERGE 1
+#endif
+constexpr bool kHalfMerge = VAME_HALF_MERGE != 0;
+
 // where affine_me_quad runs beside the 128-class kernels (VAME_Q1_SIDE
 // timing builds: 1 = after affine_me_quad2 on the quadrant stream)
 #ifndef VAME_Q1_SIDE
 #define VAME_Q1_SIDE 0
 #endif
-constexpr bool kQ1Side = VAME_Q1_SIDE != 0;
-// VAME_SPLIT=0 timing builds: every quadrant CU in affine_me_quad (the
-// packing of rounds 4-5, which PROF keeps)
+constexpr bool kQ1Side = VAME_Q1_SIDE == 1;  // 2: on a second side stream
+// The quadrant kernels, by launch mode (default, VAME_SPLIT=3): a 2-CP-only
+// launch runs one affine_me_quad kernel over the SBL1 and SBL2 items (the
+// short c2 step needs the two kinds of items side by side: c2 0.889 vs
+// 0.953 ms as two kernels), a 2+3-CP launch the SBL2 items in affine_me_quad2
+// on the quadrant stream beside affine_me_quad with the SBL1 items on the
+// caller's stream (c4 291.3 vs 298.8 ms in one kernel, whose two bodies
+// spill more: 104 vs 28 B per lane), profiles/r06_quad2_ab.txt.  Timing
+// builds: 2 / 1 one structure for every mode, 0 every quadrant CU one
+// sub-block per lane (the packing of rounds 4-5, which PROF keeps).
 #ifndef VAME_SPLIT
-#define VAME_SPLIT 1
+#define VAME_SPLIT 3
 #endif
-constexpr bool kSplit = VAME_SPLIT != 0;
 
 // The launches of one call.  By default (VAME_STREAMS=2) the 128-class
 // kernels run on the caller's stream and the quadrant kernel on a side stream
@@ -592,11 +613,16 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
       VAME_HIP(hipEventRecord(c->evJoin, c->side));
       VAME_HIP(hipStreamWaitEvent(stream, c->evJoin, 0));
     }
+    if (c->side2) {
+      VAME_HIP(hipEventRecord(c->evJoin2, c->side2));
+      VAME_HIP(hipStreamWaitEvent(stream, c->evJoin2, 0));
+    }
     return VAME_OK;
   };
   if (fork) {
     VAME_HIP(hipEventRecord(c->evFork, stream));
     VAME_HIP(hipStreamWaitEvent(c->side, c->evFork, 0));
+    if (c->side2) VAME_HIP(hipStreamWaitEvent(c->side2, c->evFork, 0));
   }
   // the 128x128 CUs: affine_me_ctu2 (two sub-blocks per lane), under PROF
   // affine_me_ctu_prof
@@ -630,6 +656,18 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
       VAME_TRY(events(2, t0, t1));
       VAME_HIP(launch_kernel(kernel_for<kKindHalf>(mode), grid, Cfg<kKindHalf>::THREADS, stream, t0, t1,
                              order_flag(), kh, capture));
+      return VAME_OK;
+    }
+    if (kHalfMerge) {  // one launch over both orientations: dHalfW then dHalfH, adjacent
+      KParams kh = kp;
+      kh.items = c->dHalfW;
+      kh.nItems = c->nHalfW + c->nHalfH;
+      kh.bestS = c->bestS + c->bestOff[1];  // [pair, CTU, item of 4]: the two regions' span
+      const unsigned grid = block_grid(c, 1, kh);
+      hipEvent_t t0, t1;
+      VAME_TRY(events(4, t0, t1));
+      VAME_HIP(launch_kernel(kernel_for<kKindHalf2W + 100>(mode), grid, Cfg<kKindHalf2W>::THREADS, stream, t0,
+                             t1, order_flag(), kh, capture));
       return VAME_OK;
     }
     for (int o = 0; o < 2; o++) {
@@ -668,8 +706,10 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
   // the split packing: affine_me_quad2 on the quadrant stream, affine_me_quad
   // after the 128-class kernels on the caller's stream (one stream: both
   // quadrant kernels first)
+  const bool kSplit = VAME_SPLIT == 1 || (VAME_SPLIT == 3 && mode != 1);  // the SBL2 items apart
   auto quads = [&](const KParams& kp, hipStream_t s1) -> int {
-    if (c->prof || !kSplit) return quad(kp, 2, sQuad);
+    if (c->prof || VAME_SPLIT == 0) return quad(kp, 2, sQuad);
+    if (!kSplit) return quad(kp, 3, sQuad);
     VAME_TRY(quad(kp, 1, sQuad));
     if (s1 == sQuad || !fork) VAME_TRY(quad(kp, 0, s1));
     return VAME_OK;
@@ -683,7 +723,7 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
       }
       if (fork) {
         VAME_TRY(quads(kp, kQ1Side ? sQuad : stream));
-        if (!kQ1Side && !c->prof && kSplit) VAME_TRY(quad(kp, 0, stream));
+        if (!kQ1Side && !c->prof && kSplit) VAME_TRY(quad(kp, 0, c->side2 ? c->side2 : stream));
       }
     }
     return fork ? join() : VAME_OK;
@@ -769,9 +809,21 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   DeviceGuard guard(device);
   VAME_HIP(guard.err);
   std::vector<Item> big1, hf, bigP, hfP;
-  QuadSet qs[3];  // affine_me_quad, affine_me_quad2; the PROF packing
+  QuadSet qs[4];  // SBL1 items, SBL2 items; the PROF packing; the product's merged set
   build_templates(big1, hf, qs[0], &qs[1]);
   build_templates(bigP, hfP, qs[2], nullptr);
+  // one affine_me_quad launch over both: the cooperative (64x64) items first,
+  // then the SBL2 items, then the 16-sub-block items (the shortest last)
+  for (int a = 0; a < 3; a++) {
+    const std::vector<Item>& v1 = a == 0 ? qs[0].full : a == 1 ? qs[0].half : qs[0].both;
+    const std::vector<Item>& v2 = a == 0 ? qs[1].full : a == 1 ? qs[1].half : qs[1].both;
+    std::vector<Item>& m = a == 0 ? qs[3].full : a == 1 ? qs[3].half : qs[3].both;
+    for (const Item& it : v1)
+      if (it.coop & 1) m.push_back(it);
+    m.insert(m.end(), v2.begin(), v2.end());
+    for (const Item& it : v1)
+      if (!(it.coop & 1)) m.push_back(it);
+  }
   std::vector<Item> hfw, hfh;  // the single-CU half items by orientation
   for (const Item& it : hf) (it.cu[0].lw > it.cu[0].lh ? hfw : hfh).push_back(it);
   // the kernels index bestS by these counts (best_layout); the templates hold
@@ -788,7 +840,7 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   c->nHalfW = (int)hfw.size();
   c->nHalfH = (int)hfh.size();
   std::vector<Item> quad;  // [set][FULL | HALF | both alignments]
-  for (int k = 0; k < 3; k++)
+  for (int k = 0; k < 4; k++)
     for (int a = 0; a < 3; a++) {
       const std::vector<Item>& v = a == 0 ? qs[k].full : a == 1 ? qs[k].half : qs[k].both;
       c->quadOff[k][a] = (int)quad.size();
@@ -808,8 +860,12 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   upload(c->dQuad, quad);
   upload(c->dBig1, big1);
   upload(c->dHalf, hf);
-  upload(c->dHalfW, hfw);
-  upload(c->dHalfH, hfh);
+  {  // the 128x64 items, then the 64x128 ones, adjacent (affine_me_half2 runs both)
+    std::vector<Item> hwh(hfw);
+    hwh.insert(hwh.end(), hfh.begin(), hfh.end());
+    upload(c->dHalfW, hwh);
+    if (c->dHalfW) c->dHalfH = c->dHalfW + hfw.size();
+  }
   for (int k = 0; k < 2 && e == hipSuccess; k++) {
     const std::vector<int32_t> order = build_order(nCtus, c->ctusPerRow, c->groupCombos[k], c->nChunks[k], c->cpp[k]);
     e = hipMalloc(&c->dOrder[k], order.size() * sizeof(int32_t));
@@ -823,7 +879,10 @@ int vame_create(vame_ctx** out, int device, int width, int height) {
   // caller's own copy streams on the quadrant kernel's queue (the CLI's
   // compute, upload and download streams + the side stream are four)
   if (e == hipSuccess && c->streams == 2) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  if (e == hipSuccess && c->streams == 2 && VAME_SPLIT != 2 && VAME_Q1_SIDE == 2)
+    e = hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evJoin2, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bestEv, hipEventDisableTiming);
   if (e == hipSuccess && c->valueSync) {
@@ -864,13 +923,14 @@ int vame_get_max_pairs(vame_ctx* c) { return c ? c->maxPairs : VAME_E_INVALID; }
 void vame_destroy(vame_ctx* c) {
   if (!c) return;
   DeviceGuard guard(c->device);
-  for (Item* d : {c->dQuad, c->dBig1, c->dHalf, c->dHalfW, c->dHalfH})
+  for (Item* d : {c->dQuad, c->dBig1, c->dHalf, c->dHalfW})  // dHalfH lies inside dHalfW's block
     if (d) (void)hipFree(d);
   if (c->bestS) (void)hipFree(c->bestS);
   for (int k = 0; k < 2; k++)
     if (c->dOrder[k]) (void)hipFree(c->dOrder[k]);
   if (c->side) (void)hipStreamDestroy(c->side);
-  for (hipEvent_t e : {c->evJoin, c->evFork, c->bestEv, c->packEv})
+  if (c->side2) (void)hipStreamDestroy(c->side2);
+  for (hipEvent_t e : {c->evJoin, c->evJoin2, c->evFork, c->bestEv, c->packEv})
     if (e) (void)hipEventDestroy(e);
   if (c->syncWord) (void)hipFree(c->syncWord);
   if (c->dPackSegs) (void)hipFree(c->dPackSegs);

@@ -70,7 +70,8 @@ static_assert(sizeof(CuSlot) == 8, "CuSlot packing");
 struct Item {
   int16_t nCu;      // CU slots (host view; unused slots have lw 0)
   int16_t rx, ry;   // region origin (CTU-relative)
-  int16_t coop;     // bit 0: cooperative (a task's CUs span waves); bit 1: autonomous waves claim tasks
+  int16_t coop;     // bit 0: cooperative (a task's CUs span waves); bit 1: autonomous waves claim tasks;
+                    // bit 2: two stacked sub-blocks per lane (affine_me_quad's SBL2 items)
   int16_t nTasks;
   int16_t rw, rh;   // affine_me_half items: the region's extent (the CU's); 0 elsewhere
   int16_t pad;
@@ -1487,38 +1488,69 @@ __device__ __forceinline__ void reduce_equations(const int (&S)[SBL][5], int u, 
 }
 
 
+// The LDS of one work item (a kernel's workgroup), laid out for kernel class
+// KIND (BEST: a 2-CP pass feeds a 3-CP pass, MODE 3).  A kernel entry declares
+// it; the quadrant kernel's bodies for one and for two sub-blocks per lane
+// share one (affine_me_quad).  Members ordered by alignment (no padding: four
+// quadrant workgroups need <= 40,960 B each).
+template <int KIND, bool BEST>
+struct Lds {
+  using C = Cfg<KIND>;
+  static constexpr int SBL = C::SBL;
+  static constexpr bool STASH = SBL == 2 && C::STASH;
+  alignas(16) uint16_t tile[C::TILE_ELEMS];
+  uint4 coef[48];
+  long long val[C::MAXCU][kNumMom];
+  double mat[C::MAXCU][42];  // per CU: N x (N + 1) system, N <= 6
+  CuState st[C::MAXCU];
+  // row 0 / row 3 of every lane's prediction (packed pairs): of its sub-block,
+  // or with two stacked sub-blocks per lane (SBL = 2) the upper one's top and
+  // the lower one's bottom row (their inner rows stay in the lane)
+  uint2 top[C::THREADS];
+  uint2 bot[C::THREADS];
+  // SBL = 2: the upper sub-block's prediction, parked in LDS from its SATD to
+  // the gradient step (row r of lane t at [r][t]), so the lower one's
+  // prediction runs with no extra live registers
+  uint2 pred[STASH ? 4 : 1][STASH ? C::THREADS : 1];
+  CuSlot cu[C::ITEMCU];
+  // the five gradient sums of every sub-block at its CU's best 2-CP iteration
+  // (3-CP seed reuse, see the 3-CP init); SBL = 2 keeps them in p.bestS
+  int bestS[5][SBL == 1 && BEST ? C::NSB : 1];
+  int hdr[2];  // item header, next wave task to claim
+  uint8_t eqmap[76];  // EqMap entries 0..73
+};
+
 // MODE (one kernel per launch mode, so each holds only the pass copies it
 // runs): 1 = 2-CP only, 2 = 3-CP only (seeds from p.prev), 3 = 2-CP then 3-CP.
-template <int KIND, bool PROF, int MODE>
-__device__ __forceinline__ void affine_me_body(const KParams& p) {
+// L: the work item's LDS (Lds<KIND>, or a layout that holds it).
+template <int KIND, bool PROF, int MODE, typename L>
+__device__ __forceinline__ void affine_me_body(const KParams& p, L& lds) {
   constexpr bool run2 = (MODE & 1) != 0, run3 = (MODE & 2) != 0;
   using C = Cfg<KIND>;
   constexpr int REGION = C::REGION;  // instrumentation slots: 128 = the 128-class kernels
   (void)REGION;
-  __shared__ __attribute__((aligned(16))) uint16_t s_tile[C::TILE_ELEMS];
   static_assert((C::TP * 2) % 16 == 0 && C::TILE_W % 8 == 0, "16-byte tile rows");
-  // row 0 / row 3 of every lane's prediction (packed pairs): of its sub-block,
-  // or with two stacked sub-blocks per lane (SBL = 2) the upper one's top and
-  // the lower one's bottom row (their inner rows stay in the lane)
-  __shared__ uint2 s_top[C::THREADS];
-  __shared__ uint2 s_bot[C::THREADS];
-  // the five gradient sums of every sub-block at its CU's best 2-CP iteration
-  // (3-CP seed reuse, see the 3-CP init); SBL = 2 keeps them in p.bestS
   constexpr int SBL = C::SBL;
-  __shared__ int s_bestS[5][SBL == 1 ? C::NSB : 1];
-  // SBL = 2: the upper sub-block's prediction, parked in LDS from its SATD to
-  // the gradient step (row r of lane t at [r][t]), so the lower one's
-  // prediction runs with no extra live registers
   constexpr bool STASH = SBL == 2 && C::STASH;
-  __shared__ uint2 s_pred[STASH ? 4 : 1][STASH ? C::THREADS : 1];
-  __shared__ __attribute__((aligned(16))) long long s_val[C::MAXCU][kNumMom];
-  __shared__ double s_mat[C::MAXCU][42];  // per CU: N x (N + 1) system, N <= 6
-  __shared__ __attribute__((aligned(16))) uint4 s_coef[48];
-  __shared__ uint8_t s_eqmap[80];
-  __shared__ CuState s_st[C::MAXCU];
-  __shared__ CuSlot s_cu[C::ITEMCU];
-  __shared__ int s_hdr[2];  // item header, next wave task to claim
-  __shared__ long long s_dup[(VAME_DUP & 4) ? kNumMom : 1];
+  using Own = Lds<KIND, run2 && run3>;  // the layout this body needs: L's arrays are at least as large
+  static_assert(sizeof(L::tile) >= sizeof(Own::tile) && sizeof(L::top) >= sizeof(Own::top) &&
+                    sizeof(L::bestS) >= sizeof(Own::bestS) && sizeof(L::pred) >= sizeof(Own::pred) &&
+                    sizeof(L::val) >= sizeof(Own::val) && sizeof(L::mat) >= sizeof(Own::mat) &&
+                    sizeof(L::st) >= sizeof(Own::st) && sizeof(L::cu) >= sizeof(Own::cu),
+                "LDS layout too small for this kernel class");
+  uint16_t* s_tile = lds.tile;
+  uint2* s_top = lds.top;
+  uint2* s_bot = lds.bot;
+  auto& s_bestS = lds.bestS;
+  auto& s_pred = lds.pred;
+  auto& s_val = lds.val;
+  auto& s_mat = lds.mat;
+  uint4* s_coef = lds.coef;
+  uint8_t* s_eqmap = lds.eqmap;
+  CuState* s_st = lds.st;
+  CuSlot* s_cu = lds.cu;
+  int* s_hdr = lds.hdr;
+  __shared__ long long s_dup[(VAME_DUP & 4) ? kNumMom : 1];  // timing-only builds
 
   const int tid = threadIdx.x;
   [[maybe_unused]] const int lane = tid & 63;  // (the phase-timing macros)
@@ -1608,7 +1640,7 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   }
   if (tid < C::ITEMCU) s_cu[tid] = it->cu[tid];
   if (tid < 48) s_coef[tid] = reinterpret_cast<const uint4*>(&kCoefTab)[tid];
-  if (tid < 80) s_eqmap[tid] = kEqMap.v[tid];
+  if (tid < 76) s_eqmap[tid] = kEqMap.v[tid];
   if (tid == 0) {
     s_hdr[0] = it->coop | (it->nTasks << 16);
     s_hdr[1] = 4;  // tasks 0 .. 3: waves 0 .. 3
@@ -2225,52 +2257,85 @@ __device__ __forceinline__ void affine_me_body(const KParams& p) {
   PC_FLUSH
 }
 
-// Distinct entry points so profiles tell the two work-item classes apart.
-// Quadrant items: 4 workgroups per CU fit the LDS (~40 KB each), so cap the
-// VGPRs at 128 to let all 16 waves be resident.
+// Distinct entry points so profiles tell the work-item classes apart.
+// Quadrant items: 4 workgroups per CU fit the LDS (~36-41 KB each), so cap the
+// VGPRs at 128 to let all 16 waves be resident.  An item flagged SBL2 (Item
+// coop bit 2: the CUs of 32-128 sub-blocks) runs the body with two stacked
+// sub-blocks per lane, the others (16-sub-block and 64x64 CUs) with one; both
+// bodies share the workgroup's LDS (one Lds<kKindQuad, ...>).
+__device__ __forceinline__ bool quad_item_sbl2(const KParams& p) {
+  const int b = blockIdx.x;
+  const int gr = b % (p.nItems * p.groupPer);
+  return (p.items[gr / p.groupPer].coop & 4) != 0;
+}
 template <int MODE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad(
     KParams p) {
-  affine_me_body<kKindQuad, false, MODE>(p);
+  __shared__ Lds<kKindQuad, MODE == 3> lds;
+  if (quad_item_sbl2(p))
+    affine_me_body<kKindQuad2, false, MODE>(p, lds);
+  else
+    affine_me_body<kKindQuad, false, MODE>(p, lds);
 }
-// The quadrant CUs of 32 to 128 sub-blocks, two stacked sub-blocks per lane
-// (autonomous wave tasks only): 4 workgroups per CU, 128 VGPRs.
+// Timing builds (VAME_SPLIT=1): the SBL2 items as a kernel of their own.
 template <int MODE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad2(
     KParams p) {
-  affine_me_body<kKindQuad2, false, MODE>(p);
+  __shared__ Lds<kKindQuad2, MODE == 3> lds;
+  affine_me_body<kKindQuad2, false, MODE>(p, lds);
 }
 // ONE 128x128 CU per 512-thread workgroup, two stacked sub-blocks per lane,
 // two workgroups per CU (~72 KB of LDS each; the 3-CP seed-reuse sums in
 // global memory): 128 VGPRs so both fit.
 template <int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_ctu2(KParams p) {
-  affine_me_body<kKindCtu2, false, MODE>(p);
+  __shared__ Lds<kKindCtu2, MODE == 3> lds;
+  affine_me_body<kKindCtu2, false, MODE>(p, lds);
 }
 // ONE 128x64 (w) / 64x128 (h) CU per 256-thread workgroup, two stacked
 // sub-blocks per lane, four workgroups per CU (~40 KB of LDS each).
 template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_half2w(KParams p) {
-  affine_me_body<kKindHalf2W, false, MODE>(p);
+  __shared__ Lds<kKindHalf2W, MODE == 3> lds;
+  affine_me_body<kKindHalf2W, false, MODE>(p, lds);
 }
 template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_half2h(KParams p) {
-  affine_me_body<kKindHalf2H, false, MODE>(p);
+  __shared__ Lds<kKindHalf2H, MODE == 3> lds;
+  affine_me_body<kKindHalf2H, false, MODE>(p, lds);
 }
-// The same with PROF (vame_set_prof): the quadrant items; the 128x128 CU in
-// one 1024-thread workgroup per CU (~100 KB of LDS), one lane per sub-block;
-// each 128x64 / 64x128 CU in a 512-thread workgroup, two per CU (~74 KB of
-// LDS each).
+// Both orientations in one launch (an item's region width tells which), so
+// the 128x64 and 64x128 CUs run side by side instead of one kernel after the
+// other on the stream; the 64x128 layout's LDS holds the 128x64 one's.
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_half2(KParams p) {
+  __shared__ Lds<kKindHalf2H, MODE == 3> lds;
+  const int gr = blockIdx.x % (p.nItems * p.groupPer);
+  const Item& it = p.items[gr / p.groupPer];
+  if (it.rw > it.rh)
+    affine_me_body<kKindHalf2W, false, MODE>(p, lds);
+  else
+    affine_me_body<kKindHalf2H, false, MODE>(p, lds);
+}
+// The same with PROF (vame_set_prof): the quadrant items (one sub-block per
+// lane, every quadrant CU); the 128x128 CU in one 1024-thread workgroup per
+// CU (~100 KB of LDS), one lane per sub-block; each 128x64 / 64x128 CU in a
+// 512-thread workgroup, two per CU (~74 KB of LDS each).
 template <int MODE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad_prof(
     KParams p) {
-  affine_me_body<kKindQuad, true, MODE>(p);
+  __shared__ Lds<kKindQuad, MODE == 3> lds;
+  affine_me_body<kKindQuad, true, MODE>(p, lds);
 }
 template <int MODE>
-__global__ __launch_bounds__(1024) void affine_me_ctu_prof(KParams p) { affine_me_body<kKindCtu, true, MODE>(p); }
+__global__ __launch_bounds__(1024) void affine_me_ctu_prof(KParams p) {
+  __shared__ Lds<kKindCtu, MODE == 3> lds;
+  affine_me_body<kKindCtu, true, MODE>(p, lds);
+}
 template <int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_half_prof(KParams p) {
-  affine_me_body<kKindHalf, true, MODE>(p);
+  __shared__ Lds<kKindHalf, MODE == 3> lds;
+  affine_me_body<kKindHalf, true, MODE>(p, lds);
 }
 
 }  // namespace vame
