@@ -10,9 +10,11 @@ import sys
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
 for c in sys.argv[2:]:
-    O = os.path.join(R, "gpurun_out", f"prof_{c}")
+    O = os.path.join(R, "gpurun_out", f"prof_{tag}_{c}")  # run_profile.sh <tag>_<config> <config>
+    if not os.path.isdir(O):
+        O = os.path.join(R, "gpurun_out", f"prof_{c}")
     s = json.load(open(os.path.join(O, "summary.json")))
-    s["source"] = f"gpurun_out/prof_{c} (profiles/run_profile.sh {c} {c}, {tag})"
+    s["source"] = f"{os.path.relpath(O, R)} (profiles/run_profile.sh, {tag})"
     json.dump(s, open(os.path.join(R, "profiles", f"pmc_{c}.json"), "w"), indent=1)
     shutil.copy(os.path.join(O, "trace", "run_kernel_stats.csv"), os.path.join(R, "profiles", f"{tag}_{c}_kernel_stats.csv"))
     shutil.copy(os.path.join(O, "count.json"), os.path.join(R, "profiles", f"{tag}_{c}_pred_count.json"))

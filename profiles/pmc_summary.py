@@ -85,16 +85,21 @@ def timed_dispatches(d):
     P = (line.get("prewarm") or {}).get("steps", 0)
     roof = line["roofline"]
     ts = roof.get("timed_sample") or {}
-    lps = ts.get("launches_per_step")  # the quadrant kernel's launches per step (sampled events)
-    launches = {"affine_me_quad": roof.get("launches")}
-    events = {"affine_me_quad": roof.get("avg_launch_ms")}
-    for k in ("affine_me_ctu", "affine_me_half", "affine_me_ctu2", "affine_me_half2w",
-              "affine_me_half2h"):  # the 128-class kernels (timed on their own steps)
-        launches[k] = roof.get(k, {}).get("launches")
-        events[k] = roof.get(k, {}).get("avg_launch_ms")
+    lps = ts.get("launches_per_step")  # the quadrant kernels' launches per step (sampled events)
+    dom = roof.get("kernel", "affine_me_quad")  # the line's dominant kernel
+    launches = {dom: roof.get("launches")}
+    events = {dom: roof.get("avg_launch_ms")}
+    for k in ("affine_me_quad", "affine_me_ctu", "affine_me_half", "affine_me_ctu2", "affine_me_half2",
+              "affine_me_half2w", "affine_me_half2h"):  # the others beside it
+        if k != dom:
+            launches[k] = roof.get(k, {}).get("launches")
+            events[k] = roof.get(k, {}).get("avg_launch_ms")
+    # the quadrant kernels carry events in the sampled timed steps; the
+    # 128-class kernels are timed on their own steps after them
+    sampled = {dom} | {k for k in launches if (roof.get(k) or {}).get("timed_on") == "the sampled timed steps"}
     out = {}
     for k, L in launches.items():
-        if k == "affine_me_quad" and lps:  # every timed dispatch, sampled events or not
+        if k in sampled and lps:  # every timed dispatch, sampled events or not
             L = lps * K
         if not L or L % K or k not in per:
             continue
@@ -146,6 +151,8 @@ def main():
                                           ("wait_any", "SQ_WAIT_ANY")) if c in sqm}
         res["kernels"][k] = e
     timed, events, line = timed_dispatches(d)
+    dom = ((line or {}).get("roofline") or {}).get("kernel", "affine_me_quad")
+    res["dominant_kernel"] = dom
     if line is not None:  # the workload the profile was taken on (bench.py checks it against its own)
         c = line.get("config", {})
         res["profiled_workload"] = {"resolution": c.get("resolution"), "qp": c.get("qp"),
@@ -159,7 +166,7 @@ def main():
         e["timed_dispatches"] = len(v)
         e["timed_avg_ms"] = mean(v)
         e["traced_run_event_avg_ms"] = events.get(k)
-    q = res["kernels"].get("affine_me_quad", {})
+    q = res["kernels"].get(dom, {})
     res["quad_timed_avg_ms_rocprof"] = q.get("timed_avg_ms")
     res["quad_hbm_bytes_per_launch"] = q.get("hbm_bytes_per_launch")
     res["quad_avg_ms_rocprof"] = q.get("avg_ms")

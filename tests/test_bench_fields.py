@@ -71,7 +71,8 @@ def test_committed_line_matches_profile(cfg):
     d = json.load(open(line_path))
     p = json.load(open(prof_path))
     roof = d["roofline"]
-    if not roof.get("profile_same_library"):
+    if not roof.get("profile_same_library") or \
+            (d.get("native") or {}).get("sha256") != (p.get("profiled_workload") or {}).get("native_sha256"):
         pytest.skip("the committed line ran another library than the profile")
     assert roof["bound"] == "valu" and roof["frac"] <= 1 and roof["busy"] <= 1
     q = p["kernels"][roof.get("kernel", "affine_me_quad")]
