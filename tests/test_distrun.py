@@ -20,7 +20,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from vame import distrun, shard
+from vame import distrun, logs, shard
 from vame.hostlogic import lambda_for_poc, ref_list
 from vame.synth import synth_sequence, write_csv
 
@@ -230,7 +230,6 @@ def test_rank_only_part_files_are_replaced(seq):
             "-o", str(seq / "orig.csv"), "-r", str(seq / "recon.csv"), "-l", str(out / "log"),
             "--gpus", "2", "--rank-only", "1"]
     a = distrun.parse_args(argv)
-    a.shard_logs = True
     table = torch.load(seq / "table.pt", weights_only=True)
     pre = distrun.part_prefix(a.log, 1)
     names = [os.path.basename(n) for n in __import__("vame.logs", fromlist=["x"]).log_names(pre)]
@@ -245,11 +244,58 @@ def test_rank_only_part_files_are_replaced(seq):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("world", [2, 3])
-def test_shard_logs_byte_identical(seq, world):
-    """--shard-logs: every rank writes its block, parts merged at their offsets;
-    no part file is left behind."""
-    out = run_ranks(seq, world, f"shard{world}")  # the default path
+def test_placed_logs_byte_identical(seq, world):
+    """The default path: every rank writes its block, placed at its offsets in
+    the final files; no part file is left behind."""
+    out = run_ranks(seq, world, f"place{world}")
     assert len(compare_dirs(out, seq / "expected")) == 40
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 3])
+def test_shard_logs_cat_merge_byte_identical(seq, world):
+    """--shard-logs: rank 0 writes the final files, rank k its
+    headerless part files, each as it goes; the `cat` of the parts in rank
+    order (logs.merge_parts) is the one-process logs byte for byte."""
+    out = run_ranks(seq, world, f"shard{world}", ["--shard-logs"])
+    files = sorted(os.listdir(out))
+    assert len(files) == 40 * world and sum(".part" in f for f in files) == 40 * (world - 1)
+    # the same bytes as a plain cat of rank 0's file and the parts
+    name = logs.log_names(str(out / "log"))[0]
+    cat = b"".join(open(n, "rb").read() for n in [name] + [logs.log_names(logs.part_prefix(str(out / "log"), r))[0]
+                                                            for r in range(1, world)])
+    assert logs.merge_parts(str(out / "log"), world) > 0
+    assert len(compare_dirs(out, seq / "expected")) == 40
+    assert open(name, "rb").read() == cat
+
+
+@pytest.mark.timeout(600)
+def test_shard_logs_merged_by_rank0(seq):
+    """--shard-logs --merge-parts: rank 0 appends the parts after the last rank."""
+    out = run_ranks(seq, 2, "shardmerge", ["--shard-logs", "--merge-parts"])
+    assert len(compare_dirs(out, seq / "expected")) == 40
+
+
+def test_rank_only_shard_logs_streams_its_part_files(seq):
+    """--rank-only K --shard-logs: rank K's part files are written as its
+    launches complete (no deferred rows), replace stale ones, and equal the
+    default path's part files."""
+    out = seq / "rankonly_parts"
+    out.mkdir()
+    argv = ["-f", str(SEQ["n"]), "-s", f"{SEQ['W']}x{SEQ['H']}", "-q", str(SEQ["qp"]),
+            "-o", str(seq / "orig.csv"), "-r", str(seq / "recon.csv"), "-l", str(out / "log"),
+            "--gpus", "2", "--rank-only", "1"]
+    table = torch.load(seq / "table.pt", weights_only=True)
+    names = [os.path.basename(n) for n in logs.log_names(distrun.part_prefix(str(out / "log"), 1))]
+    a = distrun.parse_args(argv)
+    distrun.run_rank(a, 2, 1, LookupEngine(a.W, a.H, table), torch.device("cpu"))
+    placed = {n: (out / n).read_bytes() for n in names}
+    for n in names:  # stale, longer than any real part
+        (out / n).write_bytes(b"X" * 1_000_000)
+    a = distrun.parse_args(argv + ["--shard-logs"])
+    assert a.log_path == "parts"
+    distrun.run_rank(a, 2, 1, LookupEngine(a.W, a.H, table), torch.device("cpu"))
+    assert {n: (out / n).read_bytes() for n in names} == placed
 
 
 def test_parse_args_rejects_bad_input():
@@ -260,6 +306,11 @@ def test_parse_args_rejects_bad_input():
     with pytest.raises(SystemExit):  # 3 pairs in 2 frames: at most 3 ranks
         distrun.parse_args(["-f", "2", "-s", "416x240", "-q", "32", "-o", "a", "-r", "b", "--gpus", "4"])
     assert distrun.parse_args(["-f", "2", "-s", "416x240", "-q", "32", "-o", "a", "-r", "b", "--gpus", "3"]).gpus == 3
+    with pytest.raises(SystemExit):  # --merge-parts needs --shard-logs
+        distrun.parse_args(["-f", "2", "-s", "416x240", "-q", "32", "-o", "a", "-r", "b", "--merge-parts"])
+    with pytest.raises(SystemExit):
+        distrun.parse_args(["-f", "2", "-s", "416x240", "-q", "32", "-o", "a", "-r", "b", "--shard-logs",
+                            "--gather-records"])
 
 
 def test_world_size_must_match_gpus(tmp_path):

@@ -511,6 +511,16 @@ std::vector<int32_t> build_order(int nCtus, int cols, int groupCombos, int& nChu
 // The kernel instance of a launch mode (vame_kernel.h MODE: 1 = 2-CP only,
 // 2 = 3-CP only, 3 = 2-CP then 3-CP).
 using KernelFn = void (*)(KParams);
+// the 128x64 and 64x128 CUs in one launch (affine_me_half2) in 2-CP-only
+// launches (c2 0.883 vs 0.888 ms), affine_me_half2w then affine_me_half2h in
+// the others (c4 290.9 vs 292.5 ms: the merged kernel's two bodies spill 88 vs
+// 20 B per lane), profiles/r06_quad2_ab.txt.  Timing builds: VAME_HALF_MERGE=2
+// merged in every mode, 0 in none.
+#ifndef VAME_HALF_MERGE
+#define VAME_HALF_MERGE 1
+#endif
+inline bool half_merged(int mode) { return VAME_HALF_MERGE == 2 || (VAME_HALF_MERGE == 1 && mode == 1); }
+
 template <int KIND>
 KernelFn kernel_for(int mode) {
   if constexpr (KIND == kKindHalf2W) {
@@ -522,7 +532,10 @@ KernelFn kernel_for(int mode) {
   } else if constexpr (KIND == kKindQuad2) {
     return mode == 1 ? affine_me_quad2<1> : mode == 2 ? affine_me_quad2<2> : affine_me_quad2<3>;
   } else if constexpr (KIND == kKindHalf2W + 100) {  // both orientations (affine_me_half2)
-    return mode == 1 ? affine_me_half2<1> : mode == 2 ? affine_me_half2<2> : affine_me_half2<3>;
+    if constexpr (VAME_HALF_MERGE == 2)
+      return mode == 1 ? affine_me_half2<1> : mode == 2 ? affine_me_half2<2> : affine_me_half2<3>;
+    else
+      return mode == 1 ? affine_me_half2<1> : nullptr;  // half_merged(): 2-CP-only launches
   } else if constexpr (KIND == kKindCtu) {  // PROF only
     return mode == 1 ? affine_me_ctu_prof<1> : mode == 2 ? affine_me_ctu_prof<2> : affine_me_ctu_prof<3>;
   } else if constexpr (KIND == kKindHalf) {  // PROF only
@@ -549,12 +562,6 @@ hipError_t launch_kernel(K kernel, unsigned grid, unsigned threads, hipStream_t 
   return hipGetLastError();
 }
 
-// the 128x64 and 64x128 CUs in one launch (affine_me_half2), or in
-// affine_me_half2w then affine_me_half2h (VAME_HALF_MERGE=0 timing builds)
-#ifndef VAME_HALF_MERGE
-#define VAME_HALF_MERGE 1
-#endif
-constexpr bool kHalfMerge = VAME_HALF_MERGE != 0;
 
 // where affine_me_quad runs beside the 128-class kernels (VAME_Q1_SIDE
 // timing builds: 1 = after affine_me_quad2 on the quadrant stream)
@@ -562,18 +569,15 @@ constexpr bool kHalfMerge = VAME_HALF_MERGE != 0;
 #define VAME_Q1_SIDE 0
 #endif
 constexpr bool kQ1Side = VAME_Q1_SIDE == 1;  // 2: on a second side stream
-// The quadrant kernels, by launch mode (default, VAME_SPLIT=3): a 2-CP-only
-// launch runs one affine_me_quad kernel over the SBL1 and SBL2 items (the
-// short c2 step needs the two kinds of items side by side: c2 0.889 vs
-// 0.953 ms as two kernels), a 2+3-CP launch the SBL2 items in affine_me_quad2
-// on the quadrant stream beside affine_me_quad with the SBL1 items on the
-// caller's stream (c4 291.3 vs 298.8 ms in one kernel, whose two bodies
-// spill more: 104 vs 28 B per lane), profiles/r06_quad2_ab.txt.  Timing
-// builds: 2 / 1 one structure for every mode, 0 every quadrant CU one
+// The quadrant kernels, by launch mode (default, VAME_SPLIT=3, vame_kernel.h
+// kQuadMerged): a 2-CP-only launch runs one affine_me_quad kernel over the
+// SBL1 and SBL2 items (the short c2 step needs the two kinds of items side by
+// side: c2 0.889 vs 0.953 ms as two kernels), a 2+3-CP launch the SBL2 items
+// in affine_me_quad2 on the quadrant stream beside affine_me_quad with the
+// SBL1 items on the caller's stream (c4 291.3 vs 298.8 ms in one kernel, whose
+// two bodies spill more: 104 vs 28 B per lane), profiles/r06_quad2_ab.txt.
+// Timing builds: 2 / 1 one structure for every mode, 0 every quadrant CU one
 // sub-block per lane (the packing of rounds 4-5, which PROF keeps).
-#ifndef VAME_SPLIT
-#define VAME_SPLIT 3
-#endif
 
 // The launches of one call.  By default (VAME_STREAMS=2) the 128-class
 // kernels run on the caller's stream and the quadrant kernel on a side stream
@@ -658,7 +662,7 @@ int launch_direct(vame_ctx* c, const std::vector<KParams>& kps, bool quadFull, b
                              order_flag(), kh, capture));
       return VAME_OK;
     }
-    if (kHalfMerge) {  // one launch over both orientations: dHalfW then dHalfH, adjacent
+    if (half_merged(mode)) {  // one launch over both orientations: dHalfW then dHalfH, adjacent
       KParams kh = kp;
       kh.items = c->dHalfW;
       kh.nItems = c->nHalfW + c->nHalfH;

@@ -2268,14 +2268,28 @@ __device__ __forceinline__ bool quad_item_sbl2(const KParams& p) {
   const int gr = b % (p.nItems * p.groupPer);
   return (p.items[gr / p.groupPer].coop & 4) != 0;
 }
+//
+// Which launch modes hand affine_me_quad SBL2 items (engine, VAME_SPLIT): by
+// default only the 2-CP-only launches; in the others the SBL2 items go to
+// affine_me_quad2 and affine_me_quad is built without the two-sub-block body,
+// whose registers would otherwise spill into the one-sub-block body too
+// (104 vs 0 B per lane in MODE 3).  Timing builds: 2 every mode, 1 / 0 none.
+#ifndef VAME_SPLIT
+#define VAME_SPLIT 3
+#endif
+template <int MODE>
+constexpr bool kQuadMerged = VAME_SPLIT == 2 || (VAME_SPLIT == 3 && MODE == 1);
 template <int MODE>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void affine_me_quad(
     KParams p) {
   __shared__ Lds<kKindQuad, MODE == 3> lds;
-  if (quad_item_sbl2(p))
-    affine_me_body<kKindQuad2, false, MODE>(p, lds);
-  else
-    affine_me_body<kKindQuad, false, MODE>(p, lds);
+  if constexpr (kQuadMerged<MODE>) {
+    if (quad_item_sbl2(p)) {
+      affine_me_body<kKindQuad2, false, MODE>(p, lds);
+      return;
+    }
+  }
+  affine_me_body<kKindQuad, false, MODE>(p, lds);
 }
 // Timing builds (VAME_SPLIT=1): the SBL2 items as a kernel of their own.
 template <int MODE>

@@ -5,14 +5,15 @@ main_aux_functions.h:387-525) -- with the POC loop cut into contiguous
 (POC, refIdx) pair blocks, one per rank (`shard.pair_shard`).
 
     python -m vame.distrun -f 240 -s 3840x2160 -q 32 -o orig.csv -r recon.csv \\
-        -l logs/out [--gpus N] [--gather-records] [--modes all|2cp] [--ExtraGradientIter E]
+        -l logs/out [--gpus N] [--shard-logs [--merge-parts] | --gather-records]
+        [--modes all|2cp] [--ExtraGradientIter E]
 
 Every rank reads only the frames its block uses (`vame_read_frames_span`,
 each launch's frames parsed just before they go up, beside the kernels of
 the launches before), codes its block in launches of up to 32 pairs
 (`vame_affine_me_batch`; the first launch small, so the GPU starts early),
 and copies each launch's results to pinned host memory while the GPU runs the
-next one.  The logs are written in the reference's order by one of two paths:
+next one.  The logs are written in the reference's order by one of three paths:
 
   default       the decision-log gather of byte counts: every rank formats
                 its own block as it completes -- rank 0 into the final files,
@@ -20,8 +21,13 @@ next one.  The logs are written in the reference's order by one of two paths:
                 the ranks gather their byte counts per file (one all_reduce,
                 RCCL) and write their blocks into the final files at their
                 offsets, all ranks in parallel (pwrite), so formatting and
-                writing scale with the ranks.  (`--shard-logs` names this path
-                too.)
+                writing scale with the ranks.
+  --shard-logs  per-rank files: rank 0 appends to the final files,
+                rank k to its own part files `<log>.partK_*` (headerless), each
+                as its launches complete, so nothing is left to write after a
+                rank's last launch.  The final files are the `cat` of rank 0's
+                and the parts in rank order (`vame.logs.merge_parts`, or
+                `--merge-parts`: rank 0 appends them after the last rank ends).
   --gather-records  the records themselves to rank 0: every other rank packs
                 its records compactly on its GPU (`shard.pack`), and after the
                 last launch one gather (RCCL over xGMI) brings them to rank 0,
@@ -70,7 +76,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--gather-records", action="store_true",
                     help="gather the decision records into rank 0, which formats the whole log")
     ap.add_argument("--shard-logs", action="store_true",
-                    help="every rank formats and places its own block (the default)")
+                    help="every rank appends its block to its own part files as it goes (<log>.partK_*)")
+    ap.add_argument("--merge-parts", action="store_true",
+                    help="with --shard-logs: rank 0 appends the part files to the final ones at the end")
     ap.add_argument("--rank-only", type=int, default=None, metavar="K",
                     help="run only rank K's share of a --gpus N job, alone on GPU 0 (no collective; "
                          "its logs stay part files): prices one rank of an N-GPU node on one GPU")
@@ -87,7 +95,9 @@ def parse_args(argv=None) -> argparse.Namespace:
         ap.error("--rank-only K needs 0 <= K < --gpus")
     if a.gather_records and a.shard_logs:
         ap.error("--gather-records and --shard-logs are two log paths: pick one")
-    a.shard_logs = not a.gather_records
+    if a.merge_parts and not a.shard_logs:
+        ap.error("--merge-parts goes with --shard-logs")
+    a.log_path = "gather" if a.gather_records else "parts" if a.shard_logs else "place"
     if shard.sequence_pairs(a.frames) < a.gpus:  # every rank codes at least one pair
         ap.error(f"--gpus {a.gpus} needs at least as many (POC, refIdx) pairs "
                  f"({shard.sequence_pairs(a.frames)} in {a.frames} frames)")
@@ -95,8 +105,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     return a
 
 
-def part_prefix(prefix: str, rank: int) -> str:
-    return f"{prefix}.part{rank}"
+part_prefix = logs.part_prefix
 
 
 def launch_batches(blocks, first: int = MAX_PAIRS):
@@ -255,22 +264,24 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
     up_th = threading.Thread(target=uploader, daemon=True)
     up_th.start()
 
-    # ---- who writes what: rank 0 appends to the final files as it goes; with
-    # --shard-logs every other rank formats its block into host memory (a
-    # deferred writer) and places it into the same files at the end.  In a
-    # one-rank process group (VAME_FORCE_PG) rank 0's own records take the
-    # gather path too, so the collective and the writing from gathered slabs
-    # run on one GPU.
-    gather_path = bool(a.log) and not a.shard_logs and dist is not None
+    # ---- who writes what: rank 0 appends to the final files as it goes; by
+    # default every other rank formats its block into host memory (a deferred
+    # writer) and places it into the same files at the end; with --shard-logs
+    # it appends to its own part files as it goes.  In a one-rank process group
+    # (VAME_FORCE_PG) rank 0's own records take the gather path too, so the
+    # collective and the writing from gathered slabs run on one GPU.
+    path = a.log_path
+    gather_path = bool(a.log) and path == "gather" and dist is not None
     self_gather = gather_path and world == 1
-    writes_own = bool(a.log) and (rank == 0 or a.shard_logs) and not self_gather
-    prefix = a.log if (rank == 0 or dist is not None) else part_prefix(a.log, rank)  # --rank-only K: parts
-    if a.log and (rank == 0 or dist is None):
-        # removeOldTraces (main.cpp:469); a --rank-only K run's part files too:
-        # the deferred writer places its rows at offsets without truncating
+    writes_own = bool(a.log) and (rank == 0 or path != "gather") and not self_gather
+    # --rank-only K (no group) and --shard-logs: rank K's rows in part files
+    prefix = a.log if rank == 0 or (dist is not None and path != "parts") else part_prefix(a.log, rank)
+    if a.log and (rank == 0 or dist is None or path == "parts"):
+        # removeOldTraces (main.cpp:469); part files too: the deferred writer
+        # places its rows at offsets without truncating, the part writer appends
         logs.remove_old(prefix)
     writer = logs.LogWriter(prefix, W, H) if (writes_own or (self_gather and rank == 0)) else None
-    if writer is not None and rank > 0:
+    if writer is not None and rank > 0 and path == "place":
         writer.defer()
     slab_parts = []
     # the compact-form check of the packed records, collected on the device and
@@ -403,9 +414,11 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
     if writer is not None and rank == 0:
         writer.close()
 
-    # ---- --shard-logs: every rank's block into the final files at its byte
-    # offsets (the sizes of the ranks before it), all ranks in parallel
-    if writer is not None and rank > 0:
+    # ---- the default path: every rank's block into the final files at its
+    # byte offsets (the sizes of the ranks before it), all ranks in parallel
+    if writer is not None and rank > 0 and path == "parts":
+        writer.close()  # its part files are complete
+    elif writer is not None and rank > 0:
         t = time.perf_counter()
         held = writer.held_sizes()
         if dist is None:  # --rank-only K: its block alone, into its part files
@@ -419,13 +432,17 @@ def run_rank(a, world: int, rank: int, engine, device, dist=None) -> dict:
         writer.flush_at(offsets)
         writer.close()
         T["merge_s"] = time.perf_counter() - t
-    elif world > 1 and a.log and a.shard_logs and dist is not None and rank == 0:
+    elif world > 1 and a.log and path == "place" and dist is not None and rank == 0:
         names = logs.log_names(a.log)
         sizes = torch.zeros((world, len(names)), dtype=torch.int64)
         sizes[0] = torch.tensor([os.path.getsize(n) if os.path.exists(n) else 0 for n in names])
         _all_reduce_cpu(dist, sizes)
-    if world > 1 and a.log and a.shard_logs and dist is not None:
-        barrier()  # every block is in place
+    if world > 1 and a.log and path != "gather" and dist is not None:
+        barrier()  # every block is in place (or in its part files)
+    if path == "parts" and a.merge_parts and rank == 0 and world > 1 and a.log:
+        t = time.perf_counter()
+        logs.merge_parts(a.log, world, pred_mask(modes))
+        T["merge_s"] = time.perf_counter() - t
     T["overall_s"] = time.perf_counter() - t_start
     return T
 
@@ -482,7 +499,7 @@ def report(a, per_rank: list[dict]) -> str:
              f"LOG_MERGE_TIME,{mx('merge_s') * 1e9:f}",
              f"LOG_BYTES,{sum(t['log_bytes'] for t in per_rank)}",
              "=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=-=",
-             "DISTRUN " + json.dumps({"ranks": len(per_rank), "shard_logs": a.shard_logs,
+             "DISTRUN " + json.dumps({"ranks": len(per_rank), "log_path": a.log_path,
                                       "per_rank": per_rank})]
     return "\n".join(lines)
 
@@ -497,7 +514,8 @@ def main(argv=None) -> int:
         dev = torch.device("cuda", 0)
         eng = Engine(a.W, a.H, 0)
         try:
-            a.shard_logs = True  # its rows stay in its own (part) files
+            if a.log_path == "gather":  # no collective: its rows stay in its own (part) files
+                a.log_path = "place"
             T = run_rank(a, a.gpus, a.rank_only, eng, dev)
         finally:
             eng.close()

@@ -5,6 +5,7 @@ frame ingest (main.cpp:293-330) and the per-CU decision log
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -84,6 +85,45 @@ def log_names(prefix: str, pred_mask: int = 15) -> list[str]:
             if name not in names:
                 names.append(name)
     return names
+
+
+def part_prefix(prefix: str, rank: int) -> str:
+    """The prefix of rank `rank`'s part files (vame.distrun --shard-logs)."""
+    return f"{prefix}.part{rank}"
+
+
+def merge_parts(prefix: str, n_parts: int, pred_mask: int = 15) -> int:
+    """Append the part files of ranks 1..n_parts-1 (headerless, in rank order)
+    to rank 0's final files and remove them: the `cat` of the parts, byte for
+    byte the one-process logs (in-kernel copies, os.copy_file_range).  Returns
+    the bytes appended."""
+    import shutil
+    finals = log_names(prefix, pred_mask)
+    parts = [log_names(part_prefix(prefix, r), pred_mask) for r in range(1, n_parts)]
+    moved = 0
+    for i, name in enumerate(finals):
+        with open(name, "ab") as dst:
+            for names in parts:
+                if not os.path.exists(names[i]):
+                    continue
+                with open(names[i], "rb") as src:
+                    left = os.fstat(src.fileno()).st_size
+                    try:
+                        while left > 0:
+                            n = os.copy_file_range(src.fileno(), dst.fileno(), left)
+                            if n <= 0:
+                                break
+                            left -= n
+                            moved += n
+                    except OSError:  # no in-kernel copy between these files
+                        pass
+                    if left > 0:
+                        src.seek(os.fstat(src.fileno()).st_size - left)
+                        dst.seek(0, os.SEEK_END)
+                        shutil.copyfileobj(src, dst, 16 << 20)
+                        moved += left
+                os.remove(names[i])
+    return moved
 
 
 def remove_old(prefix: str) -> None:
@@ -222,3 +262,11 @@ def write_poc(prefix: str, width: int, height: int, poc: int, results, nthreads:
             cost, cp = results[(r, name)]
             nb += append(prefix, m, width, height, poc, r, cost, cp, nthreads)
     return nb
+
+
+if __name__ == "__main__":  # python -m vame.logs merge <prefix> <ranks> [all|2cp]
+    import sys
+    if len(sys.argv) not in (4, 5) or sys.argv[1] != "merge":
+        sys.exit("usage: python -m vame.logs merge <log prefix> <ranks> [all|2cp]")
+    mask = 5 if len(sys.argv) == 5 and sys.argv[4] == "2cp" else 15
+    print(f"{merge_parts(sys.argv[2], int(sys.argv[3]), mask)} bytes appended")
