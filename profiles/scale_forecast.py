@@ -56,7 +56,12 @@ def main():
     # ---- frame_shard: 48 frames of 2160p, 2+3 CP
     Wf, Hf, nf = 3840, 2160, 48
     rows = sequence_pairs(nf) * pair_accounting(Wf, Hf, (2, 3))["rows"]
+    torch.cuda.init()
+    free0 = torch.cuda.mem_get_info(0)[0]
     eng = Engine(Wf, Hf, 0)
+    out["context_bytes_2160p"] = free0 - torch.cuda.mem_get_info(0)[0]  # scratch + templates, 32 pairs
+    print(f"2160p context (vame_create, 32 pairs per launch): {out['context_bytes_2160p'] / 2**20:.0f} MiB",
+          flush=True)
     for N in (1, 2, 4, 8):
         ranks = []
         for k in range(N):
@@ -81,7 +86,10 @@ def main():
             "forecast_rows_per_s": [round(rows / (s * 1e-3)) for s in reversed(span)]}
     eng.close()
     # ---- weak streams, c2: 1080p QP32, 2 frames, 2-CP, a sequence per rank
+    free0 = torch.cuda.mem_get_info(0)[0]
     eng = Engine(1920, 1080, 0)
+    out["context_bytes_1080p"] = free0 - torch.cuda.mem_get_info(0)[0]
+    print(f"1080p context: {out['context_bytes_1080p'] / 2**20:.0f} MiB", flush=True)
     for N in (1, 2, 4, 8):
         per = []
         for k in range(N):
