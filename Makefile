@@ -18,9 +18,28 @@ BINDIR  := $(PKG)/bin
 # it every kernel runs at zero scratch.
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
             -mllvm -disable-machine-licm
+# SimplifyCFG's sinking (and, for the 2-CP-only kernels, hoisting) of code
+# common to both sides of a branch stretched live ranges across the kernels'
+# per-item and per-kind branches into spill slots: without it the kernels of
+# the engine's unit drop to 0-32 B of scratch per lane and the 2-CP-only ones
+# (vame_kernels_2cp.hip) from 76-84 B to 0-40 B; c2 -2.3 %, c3 / c4 -0.8 %
+# (profiles/r06_quad2_ab.txt, seventh and eighth A/B).
+KFLAGS     := -mllvm -simplifycfg-sink-common=false
+KFLAGS_2CP := -mllvm -simplifycfg-sink-common=false -mllvm -simplifycfg-hoist-common=false
 
-LIB_SRCS := $(CSRC)/vame_engine.hip $(CSRC)/vame_hostlogic.cpp $(CSRC)/vame_io.cpp
+LIB_SRCS := $(CSRC)/vame_engine.hip $(CSRC)/vame_kernels_2cp.hip $(CSRC)/vame_hostlogic.cpp $(CSRC)/vame_io.cpp
 LIB_HDRS := $(CSRC)/vame_kernel.h $(CSRC)/vame_tables.h include/vame.h
+OBJDIR   := $(PKG)/build
+# $(call build_lib,<output .so>,<extra flags>): every unit with its own flags, then one link
+define build_lib
+	@mkdir -p $(LIBDIR) $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(2) -c -o $(OBJDIR)/$(notdir $(1)).engine.o $(CSRC)/vame_engine.hip
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS_2CP) $(2) -c -o $(OBJDIR)/$(notdir $(1)).2cp.o $(CSRC)/vame_kernels_2cp.hip
+	$(HIPCC) $(HIPFLAGS) $(2) -c -o $(OBJDIR)/$(notdir $(1)).hostlogic.o $(CSRC)/vame_hostlogic.cpp
+	$(HIPCC) $(HIPFLAGS) $(2) -c -o $(OBJDIR)/$(notdir $(1)).io.o $(CSRC)/vame_io.cpp
+	$(HIPCC) --offload-arch=$(ARCH) -fPIC -shared -o $(1) $(OBJDIR)/$(notdir $(1)).engine.o \
+	    $(OBJDIR)/$(notdir $(1)).2cp.o $(OBJDIR)/$(notdir $(1)).hostlogic.o $(OBJDIR)/$(notdir $(1)).io.o
+endef
 
 all: lib cli synth oracle probe
 
@@ -36,19 +55,16 @@ $(LIBDIR)/libvame_synth.so: $(CSRC)/vame_synth.c
 ABLATE_SET ?= 1 2 4 6 7 8 11 13 14 15 16 32
 ablate:
 	@mkdir -p $(LIBDIR)
-	for a in $(ABLATE_SET); do $(HIPCC) $(HIPFLAGS) -DVAME_ABLATE=$$a -shared -o $(LIBDIR)/libvame_ablate$$a.so $(LIB_SRCS) || exit 1; done
+	for a in $(ABLATE_SET); do $(MAKE) -s variant NAME=ablate$$a DEFS=-DVAME_ABLATE=$$a || exit 1; done
 # experiment builds: make variant NAME=x DEFS="-DFOO=1" -> lib/libvame_x.so
 variant:
-	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(LIBDIR)/libvame_$(NAME).so $(LIB_SRCS)
+	$(call build_lib,$(LIBDIR)/libvame_$(NAME).so,$(DEFS))
 # instrumentation build counting the sub-block predictions run: make count
 count:
-	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -DVAME_COUNT_PRED=1 -shared -o $(LIBDIR)/libvame_count.so $(LIB_SRCS)
+	$(call build_lib,$(LIBDIR)/libvame_count.so,-DVAME_COUNT_PRED=1)
 # profiling-only build with per-phase shader-clock counters: make phase
 phase:
-	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -DVAME_PHASE_TIMING=1 -shared -o $(LIBDIR)/libvame_phase.so $(LIB_SRCS)
+	$(call build_lib,$(LIBDIR)/libvame_phase.so,-DVAME_PHASE_TIMING=1)
 
 cli: $(BINDIR)/vame
 
@@ -58,8 +74,7 @@ tests/native/anyorder_probe: tests/native/anyorder_probe.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -Wall -o $@ $<
 
 $(LIBDIR)/libvame.so: $(LIB_SRCS) $(LIB_HDRS)
-	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(LIB_SRCS)
+	$(call build_lib,$@,)
 
 $(BINDIR)/vame: $(PKG)/host/vame_main.cpp include/vame.h $(LIBDIR)/libvame.so
 	@mkdir -p $(BINDIR)
@@ -71,10 +86,11 @@ oracle:
 	@if [ -d /root/reference ]; then $(MAKE) -s -C oracle ref; fi
 
 resource-usage:
-	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c -o /dev/null $(CSRC)/vame_engine.hip
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -Rpass-analysis=kernel-resource-usage -c -o /dev/null $(CSRC)/vame_engine.hip
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS_2CP) -Rpass-analysis=kernel-resource-usage -c -o /dev/null $(CSRC)/vame_kernels_2cp.hip
 
 clean:
-	rm -rf $(LIBDIR) $(BINDIR)
+	rm -rf $(LIBDIR) $(BINDIR) $(OBJDIR)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all lib cli synth oracle probe clean resource-usage ablate phase variant count

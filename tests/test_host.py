@@ -151,61 +151,61 @@ def test_build_record_matches_the_library():
 
 
 def kernel_scratch(lib_path):
-    """{kernel: private_segment_fixed_size} from the gfx950 code object inside
-    a built library (the clang offload bundle in its fat binary, the AMDGPU
-    metadata note read by llvm-readelf)."""
+    """{kernel: private_segment_fixed_size} from the gfx950 code objects inside
+    a built library (the clang offload bundle of each translation unit's fat
+    binary, the AMDGPU metadata note read by llvm-readelf)."""
     import struct
     import subprocess
     import tempfile
     d = open(lib_path, "rb").read()
+    out_map = {}
     i = d.find(b"__CLANG_OFFLOAD_BUNDLE__")
     assert i >= 0, "no offload bundle in " + lib_path
-    n = struct.unpack_from("<Q", d, i + 24)[0]
-    p = i + 32
-    for _ in range(n):
-        off, size, idl = struct.unpack_from("<QQQ", d, p)
-        p += 24
-        ident = d[p:p + idl].decode()
-        p += idl
-        if "gfx950" not in ident:
-            continue
-        with tempfile.NamedTemporaryFile(suffix=".co") as f:
-            f.write(d[i + off:i + off + size])
-            f.flush()
-            out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", f.name],
-                                 capture_output=True, text=True, check=True).stdout
-        names = re.findall(r"\.name:\s+(\S+)", out)
-        priv = [int(v) for v in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", out)]
-        assert len(names) == len(priv) and names
-        return dict(zip(names, priv))
-    raise AssertionError("no gfx950 code object in " + lib_path)
+    while i >= 0:
+        n = struct.unpack_from("<Q", d, i + 24)[0]
+        p = i + 32
+        for _ in range(n):
+            off, size, idl = struct.unpack_from("<QQQ", d, p)
+            p += 24
+            ident = d[p:p + idl].decode()
+            p += idl
+            if "gfx950" not in ident:
+                continue
+            with tempfile.NamedTemporaryFile(suffix=".co") as f:
+                f.write(d[i + off:i + off + size])
+                f.flush()
+                out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", f.name],
+                                     capture_output=True, text=True, check=True).stdout
+            names = re.findall(r"\.name:\s+(\S+)", out)
+            priv = [int(v) for v in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", out)]
+            assert len(names) == len(priv) and names
+            for k, v in zip(names, priv):
+                assert k not in out_map, "kernel in two units: " + k
+                out_map[k] = v
+        i = d.find(b"__CLANG_OFFLOAD_BUNDLE__", i + 32)
+    assert out_map, "no gfx950 code object in " + lib_path
+    return out_map
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-readelf"), reason="no llvm-readelf")
 def test_product_kernels_have_no_scratch():
     """zero scratch in the product kernels rests on the build's
-    -disable-machine-licm and on the kernels' opaque() recomputation, so a
-    compiler update or a kernel edit that brings spills back fails here: every
-    affine_me_* kernel of the built libvame.so has a zero private segment,
-    except the two-sub-block bodies whose upper sub-block's prediction stays in
-    registers across the lower one's: affine_me_half2w / _half2h (12-20 B per
-    lane; parked in LDS instead they ran 8 % slower, three
-    workgroups per CU instead of four), affine_me_quad2 (24-32 B; parked in
-    LDS: c4 +5 %, c2 +3 %), and the 2-CP-only kernels that carry a one- and a
-    two-sub-block body side by side, affine_me_quad<1> and affine_me_half2<1>
-    (76-84 B; the merged launches still win at c2, profiles/r06_quad2_ab.txt)
-    -- and the PROF variants (not the benchmarked path).  The 2+3-CP
-    affine_me_quad<3> (one-sub-block body only) stays within 8 B."""
+    flags (-disable-machine-licm; SimplifyCFG's common-code sinking off, and
+    for the 2-CP-only unit its hoisting too) and on the kernels' opaque()
+    recomputation, so a compiler update or a kernel edit that brings spills
+    back fails here: every affine_me_* kernel of the built libvame.so has a
+    zero private segment, except the two-sub-block quadrant bodies, whose upper
+    sub-block's prediction stays in registers across the lower one's:
+    affine_me_quad2 (16-28 B per lane; parked in LDS: c4 +5 %, c2 +3 %) and
+    the 2-CP-only affine_me_quad<1> that carries it beside the one-sub-block
+    body (40 B) -- and the PROF variants (not the benchmarked path)."""
     sizes = kernel_scratch(_lib.LIB_PATH)
     product = {k: v for k, v in sizes.items() if "affine_me" in k and "prof" not in k}
     assert len(product) == 16, sorted(product)
-    merged = ("affine_me_quadILi1E", "affine_me_half2ILi1E")
     for k, v in product.items():
-        if any(m in k for m in merged):
-            assert v <= 96, (k, v)
-        elif "half2" in k:
-            assert v <= 24, (k, v)
+        if "affine_me_quadILi1E" in k:
+            assert v <= 48, (k, v)
         elif "quad2" in k:
             assert v <= 40, (k, v)
         else:
-            assert v <= 8, (k, v)
+            assert v == 0, (k, v)

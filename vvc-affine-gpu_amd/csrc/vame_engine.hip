@@ -16,6 +16,12 @@
 #include "../../include/vame.h"
 #include "vame_kernel.h"
 
+#if VAME_SPLIT_TU
+namespace vame {
+VAME_2CP_KERNELS(extern)  // defined in vame_kernels_2cp.hip
+}
+#endif
+
 using namespace vame;
 
 static_assert(sizeof(vame_cpmvs) == 28, "Cpmvs layout (typedef.h)");

@@ -346,7 +346,7 @@ constexpr CoefTab make_coef_tab() {
   }
   return t;
 }
-__constant__ CoefTab kCoefTab = make_coef_tab();
+static __constant__ CoefTab kCoefTab = make_coef_tab();  // one copy per translation unit
 
 // ------------------------------------------------------------- motion field
 struct MvField {
@@ -1072,7 +1072,7 @@ constexpr EqMap make_eq_map() {
   for (int e = 0; e < 42; e++) m.v[32 + e] = eq_map_entry(3, e / 7, e % 7);
   return m;
 }
-__constant__ EqMap kEqMap = make_eq_map();
+static __constant__ EqMap kEqMap = make_eq_map();
 
 // Build, eliminate and back-substitute one CU's system with its segment; the
 // segment's first lane returns the deltas.  The int64 sums convert exactly
@@ -2351,5 +2351,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   __shared__ Lds<kKindHalf, MODE == 3> lds;
   affine_me_body<kKindHalf, true, MODE>(p, lds);
 }
+
+// The 2-CP-only (MODE 1) product kernels are compiled in a translation unit of
+// their own, vame_kernels_2cp.hip, whose optimisation flags suit them (the
+// Makefile); the engine's unit declares them instead of
+// instantiating them.  Instrumentation builds keep every kernel in one unit:
+// their device counters are per unit.
+#if VAME_COUNT_PRED || VAME_PHASE_TIMING
+#define VAME_SPLIT_TU 0
+#else
+#define VAME_SPLIT_TU 1
+#endif
+#define VAME_2CP_KERNELS(X)                 \
+  X template __global__ void affine_me_quad<1>(KParams);   \
+  X template __global__ void affine_me_quad2<1>(KParams);  \
+  X template __global__ void affine_me_ctu2<1>(KParams);   \
+  X template __global__ void affine_me_half2<1>(KParams);  \
+  X template __global__ void affine_me_half2w<1>(KParams); \
+  X template __global__ void affine_me_half2h<1>(KParams);
 
 }  // namespace vame
