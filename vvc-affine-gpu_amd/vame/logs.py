@@ -95,34 +95,42 @@ def part_prefix(prefix: str, rank: int) -> str:
 def merge_parts(prefix: str, n_parts: int, pred_mask: int = 15) -> int:
     """Append the part files of ranks 1..n_parts-1 (headerless, in rank order)
     to rank 0's final files and remove them: the `cat` of the parts, byte for
-    byte the one-process logs (in-kernel copies, os.copy_file_range).  Returns
-    the bytes appended."""
-    import shutil
+    byte the one-process logs.  In-kernel copies at explicit offsets
+    (os.copy_file_range; an O_APPEND descriptor would refuse them), plain
+    pread / pwrite where the file system has none.  Returns the bytes appended."""
     finals = log_names(prefix, pred_mask)
     parts = [log_names(part_prefix(prefix, r), pred_mask) for r in range(1, n_parts)]
     moved = 0
     for i, name in enumerate(finals):
-        with open(name, "ab") as dst:
+        dst = os.open(name, os.O_WRONLY | os.O_CREAT, 0o644)
+        try:
+            pos = os.fstat(dst).st_size
             for names in parts:
                 if not os.path.exists(names[i]):
                     continue
-                with open(names[i], "rb") as src:
-                    left = os.fstat(src.fileno()).st_size
+                src = os.open(names[i], os.O_RDONLY)
+                try:
+                    size, off = os.fstat(src).st_size, 0
                     try:
-                        while left > 0:
-                            n = os.copy_file_range(src.fileno(), dst.fileno(), left)
+                        while off < size:
+                            n = os.copy_file_range(src, dst, size - off, off, pos + off)
                             if n <= 0:
                                 break
-                            left -= n
-                            moved += n
+                            off += n
                     except OSError:  # no in-kernel copy between these files
                         pass
-                    if left > 0:
-                        src.seek(os.fstat(src.fileno()).st_size - left)
-                        dst.seek(0, os.SEEK_END)
-                        shutil.copyfileobj(src, dst, 16 << 20)
-                        moved += left
+                    while off < size:
+                        buf = os.pread(src, min(16 << 20, size - off), off)
+                        if not buf:
+                            raise VameError(f"short read from {names[i]}")
+                        off += os.pwrite(dst, buf, pos + off)
+                finally:
+                    os.close(src)
+                pos += size
+                moved += size
                 os.remove(names[i])
+        finally:
+            os.close(dst)
     return moved
 
 
